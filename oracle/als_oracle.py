@@ -1,0 +1,285 @@
+"""CPU oracle for the ALS hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker.  The product path
+(``als_mi355x``) never imports it and fails loudly when the HIP library is
+missing.
+
+What it restates
+----------------
+The reference (amy-leaf/Recommender-System-using-Apache-Spark-MLlib-) is one
+PySpark-2 notebook export.  Its ALS arithmetic lives in Apache Spark MLlib,
+which is *not* vendored under /root/reference and not installed here (no JVM,
+no pyspark).  Spark's version is unpinned by the reference
+(Python-2 ``0L`` literals and the ``cs100/lab4`` path date it to the
+Spark 1.3-1.6 CS100.1x era); the semantics restated below are those of
+``org.apache.spark.ml.recommendation.ALS`` (Spark >= 1.3), by symbol:
+
+* ``index_build`` / ``csr_build`` — the dense row ids and per-row rating lists
+  that ``partitionRatings`` + ``makeBlocks`` + ``UncompressedInBlock.compress``
+  produce (sorted unique src ids; every rating kept, duplicates included).
+* ``normal_equations`` — ``computeFactors`` + ``NormalEquation.add``:
+  explicit ``ata += y y^T, atb += r y`` ; implicit ``c1 = alpha |r|``,
+  ``ata += c1 y y^T``, ``atb += (1 + c1) y`` if ``r > 0``; ``numExplicits``
+  counts ratings (explicit) or ratings > 0 (implicit); implicit rows also
+  merge ``YtY`` (``computeYtY``).  All fp64 from fp32 factors.
+* ``solve`` — ``CholeskySolver.solve``: ``ata[ii] += regParam * numExplicits``
+  then LAPACK ``dppsv`` (Cholesky), result cast to Float.
+* ``train`` — ``ALS.train``'s loop: ITEMS are solved first from the user
+  factors, then users from the new item factors (the initial item factors are
+  never read).
+* ``predict`` — ``MatrixFactorizationModel.predict``: inner join on known ids,
+  fp64 dot of fp32 factors.
+* ``compute_error`` — RecommenderSystem.py:103-129 (join on (u, i), squared
+  error, reduce, count, sqrt).  Pinned by the reference's own known-answer
+  lines output.txt:16-18 (tests/golden/compute_error_kat.json).
+* ``topk`` — ``ALSModel.recommendForAll`` semantics: per row the ``top``
+  largest scores, ties broken by ascending index (build rule).
+
+Parity status: ``compute_error`` is pinned by the reference's known answers
+(output.txt:16-18).  The ALS factor / implicit / top-k arithmetic is
+**parity unpinned** by the reference itself (it holds no factors, no Spark and
+no fixture for them); it is pinned here to the restated upstream semantics and
+cross-checked against a second, independent C restatement of Spark's packed
+``dspr`` + ``dppsv`` arithmetic (oracle/als_oracle.c).
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, Sequence
+
+import numpy as np
+
+__all__ = [
+    "compute_error",
+    "index_build",
+    "csr_build",
+    "schedule_build",
+    "initialize",
+    "yty",
+    "normal_equations",
+    "solve",
+    "half_sweep",
+    "train",
+    "predict",
+    "rmse",
+    "topk",
+    "get_ratings_tuple",
+]
+
+
+# --------------------------------------------------------------------------
+# RecommenderSystem.py:16-24 — ratings line parser ("UserID::MovieID::Rating::Timestamp")
+# --------------------------------------------------------------------------
+def get_ratings_tuple(entry: str):
+    items = entry.split("::")
+    return int(items[0]), int(items[1]), float(items[2])
+
+
+# --------------------------------------------------------------------------
+# RecommenderSystem.py:103-129 — computeError
+# --------------------------------------------------------------------------
+def compute_error(predicted: Iterable[Sequence], actual: Iterable[Sequence]) -> float:
+    """sqrt(sum (act - pred)^2 / n) over the (UserID, MovieID) join.
+
+    Mirrors R:113 / R:116 (re-key by (u, i)), R:120 (join + squared error;
+    duplicate keys cross-multiply as an RDD join does), R:123 (reduce),
+    R:126 (count), R:129 (sqrt).
+    """
+    pred = {}
+    for u, i, r in predicted:
+        pred.setdefault((u, i), []).append(r)
+    sq = []
+    for u, i, r in actual:
+        for p in pred.get((u, i), ()):
+            sq.append((r - p) ** 2)
+    total = 0.0
+    for v in sq:  # reduce(lambda x, y: x + y)
+        total += v
+    return math.sqrt(float(total) / len(sq))
+
+
+# --------------------------------------------------------------------------
+# K1: dense ids + CSR (Spark makeBlocks / InBlock, restated)
+# --------------------------------------------------------------------------
+def index_build(ids: np.ndarray, id_space: int):
+    """Dense map id -> row (ascending id order), -1 when absent; plus sorted unique ids."""
+    ids = np.asarray(ids, dtype=np.int64)
+    flag = np.zeros(id_space, dtype=np.int32)
+    flag[ids] = 1
+    pos = np.cumsum(flag) - flag
+    mp = np.where(flag == 1, pos, -1).astype(np.int32)
+    uniq = np.nonzero(flag)[0].astype(np.int32)
+    return mp, uniq
+
+
+def csr_build(rows: np.ndarray, cols: np.ndarray, vals: np.ndarray, n_rows: int):
+    """Stable sort of (row, col, val) by row -> (indptr int64, indices int32, vals float32)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    order = np.argsort(rows, kind="stable")
+    counts = np.bincount(rows, minlength=n_rows).astype(np.int64)
+    indptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    return (indptr, np.asarray(cols)[order].astype(np.int32),
+            np.asarray(vals, dtype=np.float32)[order])
+
+
+def schedule_build(indptr: np.ndarray, chunk: int):
+    """The device work schedule (als_schedule_build): light rows longest first, heavy
+    rows split into chunk-sized tasks.  Returns (light, heavy, slot_begin, chunks)."""
+    deg = np.diff(indptr)
+    n = len(deg)
+    key = np.where(deg > chunk, chunk + 1, chunk - deg)
+    order = np.argsort(key, kind="stable").astype(np.int32)
+    n_heavy = int((deg > chunk).sum())
+    light = order[: n - n_heavy]
+    heavy = order[n - n_heavy:]
+    nc = (deg[heavy] + chunk - 1) // chunk
+    slot_begin = np.zeros(n_heavy + 1, dtype=np.int32)
+    np.cumsum(nc, out=slot_begin[1:])
+    chunks = []
+    for r in heavy:
+        b, e = int(indptr[r]), int(indptr[r + 1])
+        for p in range(b, e, chunk):
+            chunks.append((int(r), p, min(p + chunk, e)))
+    return light, heavy, slot_begin, chunks
+
+
+# --------------------------------------------------------------------------
+# Spark ALS.initialize: i.i.d. N(0,1) in fp32, each row scaled to unit L2 norm.
+# (Bitwise XORShiftRandom parity is out of scope: SURVEY §8f-4.)
+# --------------------------------------------------------------------------
+def initialize(n: int, k: int, seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((n, k)).astype(np.float32)
+    nrm = np.sqrt((x.astype(np.float64) ** 2).sum(axis=1, keepdims=True))
+    return (x / nrm.astype(np.float32)).astype(np.float32)
+
+
+# --------------------------------------------------------------------------
+# K2b / K2 / K3
+# --------------------------------------------------------------------------
+def yty(Y: np.ndarray) -> np.ndarray:
+    """computeYtY: sum over all src rows of y y^T in fp64."""
+    Yd = np.asarray(Y, dtype=np.float32).astype(np.float64)
+    return Yd.T @ Yd
+
+
+def normal_equations(indptr, indices, vals, Y, implicit=False, alpha=1.0, rows=None):
+    """NormalEquation.add over each dst row.  Returns (A [n,k,k], b [n,k], n_explicit [n])."""
+    Y = np.asarray(Y, dtype=np.float32)
+    k = Y.shape[1]
+    rows = np.arange(len(indptr) - 1) if rows is None else np.asarray(rows)
+    A = np.zeros((len(rows), k, k))
+    b = np.zeros((len(rows), k))
+    n_exp = np.zeros(len(rows), dtype=np.int64)
+    for t, j in enumerate(rows):
+        p0, p1 = int(indptr[j]), int(indptr[j + 1])
+        ys = Y[indices[p0:p1]].astype(np.float64)
+        r = np.asarray(vals[p0:p1], dtype=np.float32).astype(np.float64)
+        if implicit:
+            c1 = alpha * np.abs(r)
+            A[t] = (ys * c1[:, None]).T @ ys
+            b[t] = ((np.where(r > 0, 1.0 + c1, 0.0))[:, None] * ys).sum(axis=0)
+            n_exp[t] = int((r > 0).sum())
+        else:
+            A[t] = ys.T @ ys
+            b[t] = (r[:, None] * ys).sum(axis=0)
+            n_exp[t] = p1 - p0
+    return A, b, n_exp
+
+
+def solve(A, b, n_exp, reg, YtY=None):
+    """CholeskySolver.solve: A[ii] += reg * numExplicits (+ YtY for implicit), Cholesky, -> fp32."""
+    A = np.array(A, dtype=np.float64, copy=True)
+    k = A.shape[1]
+    if YtY is not None:
+        A += YtY[None]
+    A[:, np.arange(k), np.arange(k)] += reg * np.asarray(n_exp, dtype=np.float64)[:, None]
+    L = np.linalg.cholesky(A)
+    y = np.linalg.solve(L, b[..., None])
+    x = np.linalg.solve(np.transpose(L, (0, 2, 1)), y)[..., 0]
+    return x.astype(np.float32)
+
+
+def half_sweep(indptr, indices, vals, Y, reg, implicit=False, alpha=1.0, batch=4096):
+    """computeFactors for every dst row of one CSR side."""
+    n = len(indptr) - 1
+    k = np.asarray(Y).shape[1]
+    X = np.zeros((n, k), dtype=np.float32)
+    G = yty(Y) if implicit else None
+    for s in range(0, n, batch):
+        rows = np.arange(s, min(n, s + batch))
+        A, b, ne = normal_equations(indptr, indices, vals, Y, implicit, alpha, rows)
+        X[rows] = solve(A, b, ne, reg, G)
+    return X
+
+
+def train(users, items, ratings, rank, iterations, reg, implicit=False, alpha=1.0,
+          U0=None, seed=0):
+    """ALS.train: build both CSR sides, init U, then per iteration items-from-users
+    followed by users-from-items.  Returns (U, V, umap, imap, uids, iids)."""
+    users = np.asarray(users, dtype=np.int64)
+    items = np.asarray(items, dtype=np.int64)
+    ratings = np.asarray(ratings, dtype=np.float32)
+    umap, uids = index_build(users, int(users.max()) + 1)
+    imap, iids = index_build(items, int(items.max()) + 1)
+    ur, ic = umap[users], imap[items]
+    u_ptr, u_idx, u_val = csr_build(ur, ic, ratings, len(uids))
+    i_ptr, i_idx, i_val = csr_build(ic, ur, ratings, len(iids))
+    U = initialize(len(uids), rank, seed) if U0 is None else np.asarray(U0, np.float32)
+    V = np.zeros((len(iids), rank), dtype=np.float32)
+    for _ in range(iterations):
+        V = half_sweep(i_ptr, i_idx, i_val, U, reg, implicit, alpha)
+        U = half_sweep(u_ptr, u_idx, u_val, V, reg, implicit, alpha)
+    return U, V, umap, imap, uids, iids
+
+
+# --------------------------------------------------------------------------
+# K4
+# --------------------------------------------------------------------------
+def _lookup(mp, ids):
+    ids = np.asarray(ids, dtype=np.int64)
+    ok = (ids >= 0) & (ids < len(mp))
+    r = np.full(ids.shape, -1, dtype=np.int64)
+    r[ok] = mp[ids[ok]]
+    return r
+
+
+def predict(U, V, umap, imap, u, i):
+    """fp64 dot of fp32 factors; NaN for unknown ids (the mllib path drops them)."""
+    ur, ir = _lookup(umap, u), _lookup(imap, i)
+    known = (ur >= 0) & (ir >= 0)
+    out = np.full(len(ur), np.nan)
+    Ud = np.asarray(U, np.float32).astype(np.float64)
+    Vd = np.asarray(V, np.float32).astype(np.float64)
+    out[known] = (Ud[ur[known]] * Vd[ir[known]]).sum(axis=1)
+    return out
+
+
+def rmse(U, V, umap, imap, u, i, r):
+    """(sse, n) over pairs with both ids known — computeError's inner join."""
+    p = predict(U, V, umap, imap, u, i)
+    ok = ~np.isnan(p)
+    d = np.asarray(r, np.float32).astype(np.float64)[ok] - p[ok]
+    return float((d * d).sum()), int(ok.sum())
+
+
+# --------------------------------------------------------------------------
+# K5
+# --------------------------------------------------------------------------
+def topk(Q, V, top, batch=1024):
+    """Per row of Q: the `top` rows of V by score desc, ties by index asc (fp64 scores)."""
+    Q = np.asarray(Q, np.float32).astype(np.float64)
+    V = np.asarray(V, np.float32).astype(np.float64)
+    n_q, n_v = Q.shape[0], V.shape[0]
+    t = min(top, n_v)
+    idx = np.full((n_q, top), -1, dtype=np.int32)
+    sc = np.full((n_q, top), -np.inf, dtype=np.float64)
+    for s in range(0, n_q, batch):
+        S = Q[s:s + batch] @ V.T
+        ar = np.broadcast_to(np.arange(n_v), S.shape)
+        order = np.lexsort((ar, -S), axis=1)[:, :t]
+        idx[s:s + batch, :t] = order
+        sc[s:s + batch, :t] = np.take_along_axis(S, order, axis=1)
+    return idx, sc

@@ -1,0 +1,499 @@
+// K2 + K3 (+ K2b) — normal equations and Cholesky solve for one ALS half-sweep.
+//
+// Replaces, per dst row j (Spark ml/recommendation/ALS.scala, upstream):
+//   computeFactors -> NormalEquation.add   (blas.dspr + blas.daxpy, fp64)
+//                  -> CholeskySolver.solve (ata += lambda*n on the diagonal,
+//                                           LAPACK dppsv "U", fp64, result -> Float)
+//   computeYtY (implicit)                  (dspr over all src rows + treeAggregate)
+// reached from ALS.train at RecommenderSystem.py:148-149, :163, :218.
+//
+// MI355X design:
+//  * One wavefront per task.  A task is a whole "light" row (<= chunk ratings)
+//    or one chunk of a heavy row.  Rows arrive longest-first (LPT schedule).
+//  * Gram on the matrix cores: v_mfma_f32_16x16x4_f32 (exact fp32 products,
+//    k-ordered fp32 fma accumulation).  The MFMA's K dimension is the rating
+//    index: 4 ratings per instruction, lane (q = lane>>4, m = lane&15) holds
+//    factor dims m*CN .. m*CN+CN-1 of rating q, loaded straight from HBM /
+//    Infinity Cache as one float4 (a whole 256-B row per 16 lanes), so the
+//    gather needs no LDS staging.  With that dim permutation the k x k Gram is
+//    CN x CN tiles of 16x16; only the CN(CN+1)/2 upper tiles are computed
+//    (the matrix is symmetric, as Spark's packed dspr exploits).
+//  * fp32 accumulators are flushed into fp64 registers every 64 ratings, so
+//    the Gram error is that of 64-term fp32 sums, independent of row length;
+//    across blocks and across chunks accumulation is fp64 like Spark's.
+//  * The solve never leaves the CU: the fp64 Gram is packed (lower) into LDS,
+//    regularised (lambda * n on the diagonal, Spark's ALS-WR weighting), then
+//    factored by a row-per-lane fp64 Cholesky with the right-hand side carried
+//    as an augmented column, followed by a column-sweep back substitution.
+#include "als_common.h"
+
+namespace als {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kYtyChunk = 8192;      // src rows per YtY task
+
+template <int CN>
+struct Cfg {
+  static constexpr int KP = 16 * CN;                  // padded rank
+  static constexpr int NT = CN * (CN + 1) / 2;        // upper 16x16 tiles
+  static constexpr int NP = KP * (KP + 1) / 2;        // packed lower entries
+  static constexpr int SLOT = (NT * 4 + CN + 1) * 64; // doubles per partial slot
+};
+
+static inline int cn_for_k(int k) { return k <= 16 ? 1 : (k <= 32 ? 2 : 4); }
+
+template <int CN>
+__device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y)[CN]) {
+  if constexpr (CN == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
+  } else if constexpr (CN == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    y[0] = v.x; y[1] = v.y;
+  } else {
+    y[0] = *p;
+  }
+}
+
+// Accumulate the (weighted) Gram and rhs of ratings [pb, pe) of one row.
+// a64[t][r]: lane's 4 accumulator rows of upper tile t (MFMA C layout);
+// b64[c]: this lane's partial rhs for dim m*CN+c over its rating slot q
+// (summed over q by the caller).  npos: #ratings > 0 (implicit only).
+template <int CN, bool IMPLICIT, bool IDENT>
+__device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
+                                                const float* __restrict__ val, int64_t pb,
+                                                int64_t pe, const float* __restrict__ Y, int ld,
+                                                int k, float alpha,
+                                                double (&a64)[Cfg<CN>::NT][4],
+                                                double (&b64)[CN], int& npos) {
+  constexpr int NT = Cfg<CN>::NT;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int d0 = m * CN;
+  const bool dim_ok = d0 < k;
+  float dmask[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) dmask[c] = (d0 + c < k) ? 1.f : 0.f;
+
+  for (int64_t base = pb; base < pe; base += 64) {
+    const int nrem = (int)((pe - base) < 64 ? (pe - base) : 64);
+    int ci = 0;
+    float rv = 0.f;
+    if (lane < nrem) {
+      ci = IDENT ? (int)(base + lane) : col[base + lane];
+      rv = IDENT ? 1.f : val[base + lane];
+    }
+    // Issue the gathers of all 16 steps (64 ratings) before any MFMA.
+    float y[16][CN];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int src = 4 * t + q;
+      const int s = __shfl(ci, src);
+      if (src < nrem && dim_ok) {
+        load_dims<CN>(Y + (int64_t)s * ld + d0, y[t]);
+      } else {
+#pragma unroll
+        for (int c = 0; c < CN; ++c) y[t][c] = 0.f;
+      }
+    }
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float bf[CN];
+#pragma unroll
+    for (int c = 0; c < CN; ++c) bf[c] = 0.f;
+
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (g * 16 < nrem) {  // wave-uniform: skip empty 16-rating groups
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t = 4 * g + j;
+          const float r = __shfl(rv, 4 * t + q);
+          float ym[CN], ya[CN];
+          float wb;
+#pragma unroll
+          for (int c = 0; c < CN; ++c) ym[c] = y[t][c] * dmask[c];
+          if constexpr (IMPLICIT) {
+            const float c1 = alpha * fabsf(r);
+            wb = r > 0.f ? 1.f + c1 : 0.f;
+#pragma unroll
+            for (int c = 0; c < CN; ++c) ya[c] = c1 * ym[c];
+          } else {
+            wb = r;
+#pragma unroll
+            for (int c = 0; c < CN; ++c) ya[c] = ym[c];
+          }
+          int tt = 0;
+#pragma unroll
+          for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+            for (int c2 = c1; c2 < CN; ++c2) {
+              acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c1], ym[c2], acc[tt], 0, 0, 0);
+              ++tt;
+            }
+          }
+#pragma unroll
+          for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, ym[c], bf[c]);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a64[t][r] += (double)acc[t][r];
+    }
+#pragma unroll
+    for (int c = 0; c < CN; ++c) b64[c] += (double)bf[c];
+    if constexpr (IMPLICIT) npos += __popcll(__ballot(lane < nrem && rv > 0.f));
+  }
+}
+
+// Scatter the MFMA-layout Gram into the packed lower triangle in LDS.
+template <int CN>
+__device__ __forceinline__ void pack_gram(const double (&a64)[Cfg<CN>::NT][4],
+                                          double* __restrict__ P) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  int tt = 0;
+#pragma unroll
+  for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+    for (int c2 = c1; c2 < CN; ++c2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = (4 * q + r) * CN + c1, j = m * CN + c2;
+        const int hi = i > j ? i : j, lo = i > j ? j : i;
+        P[hi * (hi + 1) / 2 + lo] = a64[tt][r];
+      }
+      ++tt;
+    }
+  }
+}
+
+// Row-per-lane fp64 Cholesky of the packed matrix P (KP x KP) with the rhs
+// (b[lane]) carried as an augmented column, then back substitution.  Writes
+// x to xrow[0..ld) (zero for dims >= k).  Returns false if a pivot <= 0.
+template <int KP>
+__device__ __forceinline__ bool chol_solve(double* __restrict__ P, double* __restrict__ cb,
+                                           double b, int k, float* __restrict__ xrow, int ld) {
+  const int lane = threadIdx.x & 63;
+  const int rb = lane < KP ? lane * (lane + 1) / 2 : 0;
+  double a[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) a[j] = P[rb + j];  // entries j > lane are never used
+  double mydinv = 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int p = 0; p < KP; ++p) {
+    const double d = readlane_f64(a[p], p);
+    ok = ok && (d > 0.0);
+    const double dinv = 1.0 / sqrt(d);
+    const double l = a[p] * dinv;  // lane p: sqrt(d); lanes > p: L[lane][p]
+    if (lane >= p && lane < KP) P[rb + p] = l;  // final L, frees a[p]
+    if (lane == p) {
+      b *= dinv;
+      mydinv = dinv;
+    }
+    cb[lane] = l;
+    __syncthreads();
+    const double yp = readlane_f64(b, p);
+#pragma unroll
+    for (int j = p + 1; j < KP; ++j) a[j] = fma(-l, cb[j], a[j]);
+    if (lane > p) b = fma(-l, yp, b);
+    __syncthreads();
+  }
+  // P now holds L (packed lower); solve L^T x = y by columns.
+  double x = 0.0;
+#pragma unroll
+  for (int kk = KP - 1; kk >= 0; --kk) {
+    const int off = kk * (kk + 1) / 2;
+    const double lk = lane < kk ? P[off + lane] : 0.0;
+    const double t = b * mydinv;
+    const double xk = readlane_f64(t, kk);
+    if (lane == kk) x = xk;
+    b = fma(-lk, xk, b);
+  }
+  if (!ok) x = 0.0;
+  for (int d = lane; d < ld; d += 64) xrow[d] = (d < k) ? (float)x : 0.f;
+  return ok;
+}
+
+// Shared tail: cross-slot rhs reduce, pack, regularise, solve.
+template <int CN, bool IMPLICIT>
+__device__ __forceinline__ void finish_and_solve(double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
+                                                 int64_t n_reg, double* __restrict__ P,
+                                                 double* __restrict__ cb, int k, float reg,
+                                                 const double* __restrict__ yty,
+                                                 float* __restrict__ xrow, int ld, int row,
+                                                 int32_t* __restrict__ status) {
+  constexpr int KP = Cfg<CN>::KP, NP = Cfg<CN>::NP;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+#pragma unroll
+  for (int c = 0; c < CN; ++c) {
+    b64[c] += shfl_xor_f64(b64[c], 16);
+    b64[c] += shfl_xor_f64(b64[c], 32);
+  }
+  pack_gram<CN>(a64, P);
+  if (q == 0) {
+#pragma unroll
+    for (int c = 0; c < CN; ++c) cb[m * CN + c] = b64[c];
+  }
+  __syncthreads();
+  if constexpr (IMPLICIT) {
+    for (int e = lane; e < NP; e += 64) P[e] += yty[e];
+    __syncthreads();
+  }
+  if (lane < KP) {
+    const int di = lane * (lane + 1) / 2 + lane;
+    if (lane < k)
+      P[di] += (double)reg * (double)n_reg;
+    else
+      P[di] = 1.0;  // padded dims: identity rows, rhs 0 -> x = 0
+  }
+  const double b = lane < KP ? cb[lane] : 0.0;
+  __syncthreads();
+  const bool ok = chol_solve<KP>(P, cb, b, k, xrow, ld);
+  if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
+}
+
+template <int CN>
+__device__ __forceinline__ void store_slot(double* __restrict__ slot,
+                                           const double (&a64)[Cfg<CN>::NT][4],
+                                           const double (&b64)[CN], int npos) {
+  constexpr int NT = Cfg<CN>::NT;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = a64[t][r];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) slot[(NT * 4 + c) * 64 + lane] = b64[c];
+  slot[(NT * 4 + CN) * 64 + lane] = (double)npos;
+}
+
+template <int CN>
+__device__ __forceinline__ void add_slot(const double* __restrict__ slot,
+                                         double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
+                                         int& npos) {
+  constexpr int NT = Cfg<CN>::NT;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a64[t][r] += slot[(t * 4 + r) * 64 + lane];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) b64[c] += slot[(NT * 4 + c) * 64 + lane];
+  npos += (int)slot[(NT * 4 + CN) * 64 + lane];
+}
+
+// Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) first,
+// then whole light rows (Gram + solve fused, A never leaves the CU).
+template <int CN, bool IMPLICIT>
+__global__ __launch_bounds__(64, 2) void gram_solve_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
+    const int32_t* __restrict__ chunk_row, const int64_t* __restrict__ chunk_begin,
+    const int64_t* __restrict__ chunk_end, int32_t n_chunks, const float* __restrict__ Y,
+    float* __restrict__ X, int ld, int k, float reg, float alpha,
+    const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status) {
+  constexpr int NT = Cfg<CN>::NT;
+  __shared__ double P[Cfg<CN>::NP];
+  __shared__ double cb[64];
+  const int task = blockIdx.x;
+  double a64[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
+  double b64[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  int npos = 0;
+  if (task < n_chunks) {
+    gram_accumulate<CN, IMPLICIT, false>(col, val, chunk_begin[task], chunk_end[task], Y, ld, k,
+                                         alpha, a64, b64, npos);
+    store_slot<CN>(slots + (int64_t)task * Cfg<CN>::SLOT, a64, b64, npos);
+    return;
+  }
+  const int row = light_rows[task - n_chunks];
+  const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
+  gram_accumulate<CN, IMPLICIT, false>(col, val, pb, pe, Y, ld, k, alpha, a64, b64, npos);
+  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
+  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, P, cb, k, reg, yty, X + (int64_t)row * ld, ld,
+                                 row, status);
+}
+
+// Launch 2: heavy rows — sum their chunk slots in a fixed order, then solve.
+template <int CN, bool IMPLICIT>
+__global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
+    const int32_t* __restrict__ slot_begin, const double* __restrict__ slots,
+    float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
+    int32_t* __restrict__ status) {
+  constexpr int NT = Cfg<CN>::NT;
+  __shared__ double P[Cfg<CN>::NP];
+  __shared__ double cb[64];
+  const int h = blockIdx.x;
+  const int row = heavy_rows[h];
+  double a64[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
+  double b64[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  int npos = 0;
+  for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
+    add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
+  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
+  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, P, cb, k, reg, yty, X + (int64_t)row * ld, ld,
+                                 row, status);
+}
+
+// K2b: YtY partial Grams over row chunks of Y (unweighted, identity gather).
+template <int CN>
+__global__ __launch_bounds__(64, 2) void yty_partial_kernel(const float* __restrict__ Y, int64_t n,
+                                                            int ld, int k,
+                                                            double* __restrict__ slots) {
+  constexpr int NT = Cfg<CN>::NT;
+  double a64[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
+  double b64[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  int npos = 0;
+  const int64_t pb = (int64_t)blockIdx.x * kYtyChunk;
+  const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
+  gram_accumulate<CN, false, true>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64, b64, npos);
+  store_slot<CN>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, npos);
+}
+
+template <int CN>
+__global__ __launch_bounds__(64) void yty_reduce_kernel(const double* __restrict__ slots,
+                                                        int nslots, double* __restrict__ out) {
+  constexpr int NT = Cfg<CN>::NT, NP = Cfg<CN>::NP;
+  __shared__ double P[NP];
+  double a64[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
+  double b64[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  int npos = 0;
+  for (int s = 0; s < nslots; ++s) add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
+  pack_gram<CN>(a64, P);
+  __syncthreads();
+  for (int e = threadIdx.x; e < NP; e += 64) out[e] = P[e];
+}
+
+}  // namespace als
+
+using namespace als;
+
+extern "C" {
+
+int32_t als_k_pad(int32_t k) { return 16 * cn_for_k(k); }
+
+size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks) {
+  const int cn = cn_for_k(k);
+  const size_t slot = cn == 1 ? Cfg<1>::SLOT : (cn == 2 ? Cfg<2>::SLOT : Cfg<4>::SLOT);
+  return align_up(sizeof(double) * slot * (size_t)(n_chunks > 0 ? n_chunks : 0)) + 256;
+}
+
+int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
+                   const int32_t* light_rows, int32_t n_light, const int32_t* heavy_rows,
+                   const int32_t* heavy_slot_begin, int32_t n_heavy, const int32_t* chunk_row,
+                   const int64_t* chunk_begin, const int64_t* chunk_end, int32_t n_chunks,
+                   const float* Y_src, float* X_dst, int32_t ld, int32_t k, float reg,
+                   int implicit, float alpha, const double* yty_packed, int32_t* status_dev,
+                   void* ws, size_t ws_bytes, void* stream) {
+  ALS_REQUIRE(k >= 1 && k <= 64, ALS_EUNSUPPORTED, "als_solve_half: rank %d not in [1, 64]", k);
+  ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_solve_half: ld=%d must be >= k and %%4==0",
+              ld);
+  ALS_REQUIRE(n_light >= 0 && n_heavy >= 0 && n_chunks >= 0, ALS_EINVAL,
+              "als_solve_half: negative counts");
+  ALS_REQUIRE(Y_src && X_dst && row_ptr && status_dev, ALS_EINVAL, "als_solve_half: null pointer");
+  ALS_REQUIRE(!implicit || yty_packed, ALS_EINVAL, "als_solve_half: implicit needs yty_packed");
+  ALS_REQUIRE(reg >= 0.f && alpha >= 0.f, ALS_EINVAL, "als_solve_half: reg/alpha must be >= 0");
+  ALS_REQUIRE((reinterpret_cast<uintptr_t>(Y_src) & 15) == 0, ALS_EINVAL,
+              "als_solve_half: Y_src must be 16-byte aligned");
+  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks), ALS_EWORKSPACE,
+              "als_solve_half: workspace %zu < %zu", ws_bytes,
+              als_solve_workspace_bytes(k, n_chunks));
+  hipStream_t st = as_stream(stream);
+  double* slots = static_cast<double*>(ws);
+  const int cn = cn_for_k(k);
+  const unsigned g1 = (unsigned)(n_chunks + n_light);
+  const unsigned g2 = (unsigned)n_heavy;
+#define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
+  do {                                                                                            \
+    if (g1)                                                                                       \
+      gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
+                                                    chunk_begin, chunk_end, n_chunks, Y_src,      \
+                                                    X_dst, ld, k, reg, alpha, yty_packed, slots,  \
+                                                    status_dev);                                  \
+    ALS_LAUNCH_CHECK();                                                                           \
+    if (g2)                                                                                       \
+      reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
+                                                      slots, X_dst, ld, k, reg, yty_packed,       \
+                                                      status_dev);                                \
+    ALS_LAUNCH_CHECK();                                                                           \
+  } while (0)
+  if (implicit) {
+    if (cn == 1) ALS_SOLVE_LAUNCH(1, true);
+    else if (cn == 2) ALS_SOLVE_LAUNCH(2, true);
+    else ALS_SOLVE_LAUNCH(4, true);
+  } else {
+    if (cn == 1) ALS_SOLVE_LAUNCH(1, false);
+    else if (cn == 2) ALS_SOLVE_LAUNCH(2, false);
+    else ALS_SOLVE_LAUNCH(4, false);
+  }
+#undef ALS_SOLVE_LAUNCH
+  return ALS_OK;
+}
+
+size_t als_yty_workspace_bytes(int64_t n, int32_t k) {
+  const int64_t nslots = n > 0 ? (n + kYtyChunk - 1) / kYtyChunk : 1;
+  const int cn = cn_for_k(k);
+  const size_t slot = cn == 1 ? Cfg<1>::SLOT : (cn == 2 ? Cfg<2>::SLOT : Cfg<4>::SLOT);
+  return align_up(sizeof(double) * slot * (size_t)nslots) + 256;
+}
+
+int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed_out, void* ws,
+            size_t ws_bytes, void* stream) {
+  ALS_REQUIRE(k >= 1 && k <= 64, ALS_EUNSUPPORTED, "als_yty: rank %d not in [1, 64]", k);
+  ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_yty: bad ld");
+  ALS_REQUIRE(n >= 0 && yty_packed_out && (n == 0 || Y), ALS_EINVAL, "als_yty: bad args");
+  ALS_REQUIRE(n < (int64_t(1) << 31), ALS_EINVAL, "als_yty: n >= 2^31");
+  ALS_REQUIRE(ws_bytes >= als_yty_workspace_bytes(n, k), ALS_EWORKSPACE,
+              "als_yty: workspace too small");
+  hipStream_t st = as_stream(stream);
+  double* slots = static_cast<double*>(ws);
+  const int nslots = n > 0 ? (int)((n + kYtyChunk - 1) / kYtyChunk) : 0;
+  const int cn = cn_for_k(k);
+  if (nslots == 0) {
+    const int kp = 16 * cn;
+    ALS_HIP(hipMemsetAsync(yty_packed_out, 0, sizeof(double) * kp * (kp + 1) / 2, st));
+    return ALS_OK;
+  }
+#define ALS_YTY_LAUNCH(CN)                                                                    \
+  do {                                                                                        \
+    yty_partial_kernel<CN><<<nslots, 64, 0, st>>>(Y, n, ld, k, slots);                        \
+    ALS_LAUNCH_CHECK();                                                                       \
+    yty_reduce_kernel<CN><<<1, 64, 0, st>>>(slots, nslots, yty_packed_out);                   \
+    ALS_LAUNCH_CHECK();                                                                       \
+  } while (0)
+  if (cn == 1) ALS_YTY_LAUNCH(1);
+  else if (cn == 2) ALS_YTY_LAUNCH(2);
+  else ALS_YTY_LAUNCH(4);
+#undef ALS_YTY_LAUNCH
+  return ALS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,333 @@
+"""Device-resident ALS engine (one process per GPU).
+
+This is the host side of the hot path that replaces Spark's
+``ml.recommendation.ALS.train`` (upstream) as reached from
+RecommenderSystem.py:148-149 / :163 / :218, and ``predictAll`` +
+``computeError`` (RecommenderSystem.py:103-129, :150, :165, :222, :232).
+Every arithmetic step runs in libals_hip.so (HIP, gfx950); torch supplies
+device memory, streams and the RNG for the initial factors only.
+
+Data layout in HBM (DESIGN.md "Data layout"):
+  users/items id maps  int32[id_space]   (id -> dense row or -1)
+  user side  CSR       row_ptr int64[n_u+1], col int32[nnz] (dense item), val f32[nnz]
+  item side  CSR       row_ptr int64[n_i+1], col int32[nnz] (dense user), val f32[nnz]
+  factors              U f32[n_u, ld], V f32[n_i, ld], ld = roundup(rank, 4), pad cols 0
+  schedule per side    light rows (LPT order), heavy rows, chunk tasks
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+
+DEFAULT_CHUNK = 2048  # ratings per heavy-row task
+
+
+def ld_for(rank: int) -> int:
+    return (rank + 3) // 4 * 4
+
+
+class Workspace:
+    """One growable device scratch buffer; the library never allocates on a compute call."""
+
+    def __init__(self, device):
+        self.device = device
+        self.buf: Optional[torch.Tensor] = None
+
+    def get(self, nbytes: int) -> torch.Tensor:
+        nbytes = max(int(nbytes), 256)
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+        return self.buf
+
+
+def _to_device(x, dtype, device) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        return x.to(device=device, dtype=dtype).contiguous()
+    return torch.as_tensor(np.ascontiguousarray(np.asarray(x)), device=device).to(dtype).contiguous()
+
+
+# ---------------------------------------------------------------------------
+# K1: id maps, CSR, schedule
+# ---------------------------------------------------------------------------
+@dataclass
+class IdIndex:
+    """Dense id map of one side (the device form of Spark's sorted InBlock.srcIds)."""
+    map: torch.Tensor       # int32 [id_space]
+    uniq: torch.Tensor      # int32 [n]   ascending ids
+    n: int
+
+    @property
+    def id_space(self) -> int:
+        return int(self.map.numel())
+
+
+def build_index(ids: torch.Tensor, id_space: int, ws: Workspace) -> IdIndex:
+    L = _lib.lib()
+    dev = ids.device
+    mp = torch.empty(id_space, dtype=torch.int32, device=dev)
+    uniq = torch.empty(id_space, dtype=torch.int32, device=dev)
+    nu = torch.zeros(1, dtype=torch.int32, device=dev)
+    need = L.als_index_workspace_bytes(ids.numel(), id_space)
+    w = ws.get(need)
+    check(L.als_index_build(ptr(ids), ids.numel(), id_space, ptr(mp), ptr(uniq), ptr(nu), ptr(w),
+                            w.numel(), stream_ptr(dev)), "als_index_build")
+    n = int(nu.item())
+    return IdIndex(mp, uniq[:n].clone(), n)
+
+
+@dataclass
+class RatingBlock:
+    """One side's ratings in HBM as CSR plus its half-sweep work schedule."""
+    n_rows: int
+    nnz: int
+    row_ptr: torch.Tensor
+    col: torch.Tensor
+    val: torch.Tensor
+    chunk: int
+    n_light: int
+    n_heavy: int
+    n_chunks: int
+    light_rows: torch.Tensor
+    heavy_rows: torch.Tensor
+    heavy_slot_begin: torch.Tensor
+    chunk_row: torch.Tensor
+    chunk_begin: torch.Tensor
+    chunk_end: torch.Tensor
+
+
+def build_block(row_ids: torch.Tensor, row_index: IdIndex, col_ids: torch.Tensor,
+                col_index: IdIndex, vals: torch.Tensor, ws: Workspace,
+                chunk: int = DEFAULT_CHUNK) -> RatingBlock:
+    L = _lib.lib()
+    dev = row_ids.device
+    nnz = int(row_ids.numel())
+    n_rows = row_index.n
+    row_ptr = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
+    col = torch.empty(nnz, dtype=torch.int32, device=dev)
+    val = torch.empty(nnz, dtype=torch.float32, device=dev)
+    w = ws.get(L.als_csr_workspace_bytes(nnz, n_rows))
+    check(L.als_csr_build(ptr(row_ids), ptr(row_index.map), ptr(col_ids), ptr(col_index.map),
+                          ptr(vals), nnz, n_rows, ptr(row_ptr), ptr(col), ptr(val), ptr(w),
+                          w.numel(), stream_ptr(dev)), "als_csr_build")
+    return schedule_block(n_rows, nnz, row_ptr, col, val, ws, chunk)
+
+
+def schedule_block(n_rows, nnz, row_ptr, col, val, ws: Workspace, chunk: int = DEFAULT_CHUNK
+                   ) -> RatingBlock:
+    L = _lib.lib()
+    dev = row_ptr.device
+    counts = torch.zeros(3, dtype=torch.int32, device=dev)
+    check(L.als_schedule_count(ptr(row_ptr), n_rows, chunk, ptr(counts), stream_ptr(dev)),
+          "als_schedule_count")
+    n_light, n_heavy, n_chunks = (int(x) for x in counts.tolist())
+    i32 = dict(dtype=torch.int32, device=dev)
+    light = torch.empty(max(n_light, 1), **i32)
+    heavy = torch.empty(max(n_heavy, 1), **i32)
+    slot_begin = torch.empty(n_heavy + 1, **i32)
+    crow = torch.empty(max(n_chunks, 1), **i32)
+    cbeg = torch.empty(max(n_chunks, 1), dtype=torch.int64, device=dev)
+    cend = torch.empty(max(n_chunks, 1), dtype=torch.int64, device=dev)
+    w = ws.get(L.als_schedule_workspace_bytes(n_rows))
+    check(L.als_schedule_build(ptr(row_ptr), n_rows, chunk, n_light, n_heavy, n_chunks,
+                               ptr(light), ptr(heavy), ptr(slot_begin), ptr(crow), ptr(cbeg),
+                               ptr(cend), ptr(w), w.numel(), stream_ptr(dev)),
+          "als_schedule_build")
+    return RatingBlock(n_rows, nnz, row_ptr, col, val, chunk, n_light, n_heavy, n_chunks, light,
+                       heavy, slot_begin, crow, cbeg, cend)
+
+
+# ---------------------------------------------------------------------------
+# K2/K3/K2b
+# ---------------------------------------------------------------------------
+def k_pad(rank: int) -> int:
+    return int(_lib.lib().als_k_pad(rank))
+
+
+def compute_yty(Y: torch.Tensor, n: int, rank: int, ws: Workspace) -> torch.Tensor:
+    """fp64 YtY (lower-packed, k_pad) of the first n rows of Y."""
+    L = _lib.lib()
+    kp = k_pad(rank)
+    out = torch.empty(kp * (kp + 1) // 2, dtype=torch.float64, device=Y.device)
+    w = ws.get(L.als_yty_workspace_bytes(n, rank))
+    check(L.als_yty(ptr(Y), n, Y.shape[1], rank, ptr(out), ptr(w), w.numel(),
+                    stream_ptr(Y.device)), "als_yty")
+    return out
+
+
+def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, reg: float,
+               implicit: bool, alpha: float, yty: Optional[torch.Tensor],
+               status: torch.Tensor, ws: Workspace) -> None:
+    """One computeFactors pass: X[row] <- solve(A_row, b_row) for every row of `block`."""
+    L = _lib.lib()
+    w = ws.get(L.als_solve_workspace_bytes(rank, block.n_chunks))
+    check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
+                           ptr(block.light_rows), block.n_light, ptr(block.heavy_rows),
+                           ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),
+                           ptr(block.chunk_begin), ptr(block.chunk_end), block.n_chunks,
+                           ptr(Y), ptr(X), X.shape[1], rank, float(reg), int(bool(implicit)),
+                           float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(),
+                           stream_ptr(X.device)), "als_solve_half")
+
+
+# ---------------------------------------------------------------------------
+# K4/K5
+# ---------------------------------------------------------------------------
+def predict_pairs(u: torch.Tensor, i: torch.Tensor, uidx: IdIndex, iidx: IdIndex,
+                  U: torch.Tensor, V: torch.Tensor, rank: int) -> torch.Tensor:
+    L = _lib.lib()
+    out = torch.empty(u.numel(), dtype=torch.float64, device=U.device)
+    check(L.als_predict(ptr(u), ptr(i), u.numel(), ptr(uidx.map), uidx.id_space, ptr(iidx.map),
+                        iidx.id_space, ptr(U), ptr(V), U.shape[1], rank, ptr(out),
+                        stream_ptr(U.device)), "als_predict")
+    return out
+
+
+def rmse_pairs(u, i, r, uidx: IdIndex, iidx: IdIndex, U, V, rank: int, ws: Workspace):
+    """(sse, count) over pairs with both ids known (computeError's join)."""
+    L = _lib.lib()
+    out = torch.empty(2, dtype=torch.float64, device=U.device)
+    w = ws.get(L.als_rmse_workspace_bytes(u.numel()))
+    check(L.als_rmse_partial(ptr(u), ptr(i), ptr(r), u.numel(), ptr(uidx.map), uidx.id_space,
+                             ptr(iidx.map), iidx.id_space, ptr(U), ptr(V), U.shape[1], rank,
+                             ptr(out), ptr(w), w.numel(), stream_ptr(U.device)),
+          "als_rmse_partial")
+    return out
+
+
+def topk_rows(Q: torch.Tensor, n_q: int, V: torch.Tensor, n_v: int, rank: int, top: int):
+    """(idx int32 [n_q, top], score f32 [n_q, top]); idx = dense V row, -1 past n_v."""
+    L = _lib.lib()
+    idx = torch.empty((n_q, top), dtype=torch.int32, device=Q.device)
+    sc = torch.empty((n_q, top), dtype=torch.float32, device=Q.device)
+    check(L.als_topk(ptr(Q), n_q, ptr(V), n_v, Q.shape[1], rank, top, ptr(idx), ptr(sc), 0, 0,
+                     stream_ptr(Q.device)), "als_topk")
+    return idx, sc
+
+
+# ---------------------------------------------------------------------------
+# The engine
+# ---------------------------------------------------------------------------
+class ALSCore:
+    """Ratings, id maps, both CSR sides and both factor matrices resident on one GPU."""
+
+    def __init__(self, users, items, ratings, device=None, chunk: int = DEFAULT_CHUNK):
+        _lib.require_gpu()
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.ws = Workspace(self.device)
+        u = _to_device(users, torch.int32, self.device)
+        i = _to_device(items, torch.int32, self.device)
+        r = _to_device(ratings, torch.float32, self.device)
+        if not (u.numel() == i.numel() == r.numel()):
+            raise ValueError("users, items and ratings must have the same length")
+        if u.numel() == 0:
+            raise ValueError("ALS needs at least one rating")
+        umin, umax = int(u.min()), int(u.max())
+        imin, imax = int(i.min()), int(i.max())
+        if umin < 0 or imin < 0:
+            raise ValueError("user and item ids must be non-negative int32 values")
+        self.nnz = int(u.numel())
+        self.uidx = build_index(u, umax + 1, self.ws)
+        self.iidx = build_index(i, imax + 1, self.ws)
+        self.user_block = build_block(u, self.uidx, i, self.iidx, r, self.ws, chunk)
+        self.item_block = build_block(i, self.iidx, u, self.uidx, r, self.ws, chunk)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.U: Optional[torch.Tensor] = None
+        self.V: Optional[torch.Tensor] = None
+        self.rank = 0
+
+    @property
+    def n_users(self) -> int:
+        return self.uidx.n
+
+    @property
+    def n_items(self) -> int:
+        return self.iidx.n
+
+    # Spark ALS.initialize: unit-norm Gaussian rows, fp32.
+    def init_factors(self, rank: int, seed: int = 0, U0=None) -> None:
+        if rank < 1 or rank > 64:
+            raise ValueError(f"rank must be in [1, 64] on this build, got {rank}")
+        self.rank = rank
+        ld = ld_for(rank)
+        self.U = torch.zeros((self.n_users, ld), dtype=torch.float32, device=self.device)
+        self.V = torch.zeros((self.n_items, ld), dtype=torch.float32, device=self.device)
+        if U0 is not None:
+            U0 = _to_device(U0, torch.float32, self.device)
+            if tuple(U0.shape) != (self.n_users, rank):
+                raise ValueError(f"U0 must have shape {(self.n_users, rank)}")
+            self.U[:, :rank] = U0
+        else:
+            g = torch.Generator(device=self.device)
+            g.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
+            x = torch.randn((self.n_users, rank), generator=g, device=self.device,
+                            dtype=torch.float32)
+            self.U[:, :rank] = x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
+
+    def half_sweep_items(self, reg, implicit=False, alpha=1.0):
+        yty = compute_yty(self.U, self.n_users, self.rank, self.ws) if implicit else None
+        solve_half(self.item_block, self.U, self.V, self.rank, reg, implicit, alpha, yty,
+                   self.status, self.ws)
+
+    def half_sweep_users(self, reg, implicit=False, alpha=1.0):
+        yty = compute_yty(self.V, self.n_items, self.rank, self.ws) if implicit else None
+        solve_half(self.user_block, self.V, self.U, self.rank, reg, implicit, alpha, yty,
+                   self.status, self.ws)
+
+    def iterate(self, reg, implicit=False, alpha=1.0):
+        """One ALS iteration in Spark's order: items from users, then users from items."""
+        self.half_sweep_items(reg, implicit, alpha)
+        self.half_sweep_users(reg, implicit, alpha)
+
+    def check_status(self) -> None:
+        s = int(self.status.item())
+        if s != 0:
+            raise RuntimeError(
+                f"Cholesky failed (non-positive pivot) for dense row {s - 1}: the normal "
+                "equations are not positive definite (Spark raises from LAPACK dppsv here)")
+
+    def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0=None):
+        self.init_factors(rank, seed, U0)
+        self.status.zero_()
+        for _ in range(max_iter):
+            self.iterate(reg, implicit, alpha)
+        self.check_status()
+        return self
+
+    # ---- K4 / K5 ----
+    def predict(self, users, items) -> torch.Tensor:
+        u = _to_device(users, torch.int32, self.device)
+        i = _to_device(items, torch.int32, self.device)
+        return predict_pairs(u, i, self.uidx, self.iidx, self.U, self.V, self.rank)
+
+    def rmse(self, users, items, ratings):
+        u = _to_device(users, torch.int32, self.device)
+        i = _to_device(items, torch.int32, self.device)
+        r = _to_device(ratings, torch.float32, self.device)
+        sse, n = rmse_pairs(u, i, r, self.uidx, self.iidx, self.U, self.V, self.rank,
+                            self.ws).tolist()
+        return (math.sqrt(sse / n) if n > 0 else float("nan")), int(n)
+
+    def recommend_users(self, top: int):
+        """For every user (dense order): top items as (item ids, scores)."""
+        idx, sc = topk_rows(self.U, self.n_users, self.V, self.n_items, self.rank, top)
+        ids = torch.where(idx >= 0, self.iidx.uniq[idx.clamp(min=0).long()], idx)
+        return ids, sc
+
+    def recommend_items(self, top: int):
+        idx, sc = topk_rows(self.V, self.n_items, self.U, self.n_users, self.rank, top)
+        ids = torch.where(idx >= 0, self.uidx.uniq[idx.clamp(min=0).long()], idx)
+        return ids, sc
+
+    def user_factors(self):
+        return self.uidx.uniq, self.U[:, :self.rank]
+
+    def item_factors(self):
+        return self.iidx.uniq, self.V[:, :self.rank]

@@ -97,7 +97,10 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * into X_dst[row*ld ..].  k <= 64.  yty_packed (implicit only): lower-packed
  * fp64 k_pad x k_pad Gram from als_yty.  status_dev: device int32, set to
  * (row+1) of a row whose Cholesky pivot was not positive (0 = all rows ok;
- * Spark raises from dppsv in that case). */
+ * Spark raises from dppsv in that case).
+ * phases: bit 0 = launch 1 (heavy-row chunk partials + fused light-row
+ * gram/solve), bit 1 = launch 2 (heavy-row reduce + solve); 3 = both (the
+ * normal call; launch 2 must follow launch 1 on the same stream). */
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks);
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light,
@@ -106,7 +109,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    int32_t n_chunks,
                    const float* Y_src, float* X_dst, int32_t ld, int32_t k,
                    float reg, int implicit, float alpha, const double* yty_packed,
-                   int32_t* status_dev, void* ws, size_t ws_bytes, void* stream);
+                   int32_t* status_dev, void* ws, size_t ws_bytes, int phases, void* stream);
 
 /* K2b: YtY = sum over all n rows of Y of y y^T in fp64 (replaces Spark
  * computeYtY's dspr + treeAggregate).  Output: lower-packed fp64, k_pad(k_pad+1)/2

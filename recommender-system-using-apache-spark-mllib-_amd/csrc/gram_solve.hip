@@ -21,9 +21,9 @@
 //  * fp32 accumulators are flushed into fp64 registers every 64 ratings, so
 //    the Gram error is that of 64-term fp32 sums, independent of row length;
 //    across blocks and across chunks accumulation is fp64 like Spark's.
-//  * The solve never leaves the CU: the fp64 Gram is packed (lower) into LDS,
-//    regularised (lambda * n on the diagonal, Spark's ALS-WR weighting), then
-//    factored by a row-per-lane fp64 Cholesky with the right-hand side carried
+//  * The solve never leaves the CU: the regularised Gram is packed (lower) into LDS
+//    (lambda * n on the diagonal, Spark's ALS-WR weighting, added in fp64), then
+//    factored by a row-per-lane LDL^T with the right-hand side carried
 //    as an augmented column, followed by a column-sweep back substitution.
 #include "als_common.h"
 
@@ -83,58 +83,63 @@ __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
       ci = IDENT ? (int)(base + lane) : col[base + lane];
       rv = IDENT ? 1.f : val[base + lane];
     }
-    // Issue the gathers of all 16 steps (64 ratings) before any MFMA.
-    float y[16][CN];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int src = 4 * t + q;
-      const int s = __shfl(ci, src);
-      if (src < nrem && dim_ok) {
-        load_dims<CN>(Y + (int64_t)s * ld + d0, y[t]);
-      } else {
-#pragma unroll
-        for (int c = 0; c < CN; ++c) y[t][c] = 0.f;
-      }
-    }
     floatx4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     float bf[CN];
 #pragma unroll
     for (int c = 0; c < CN; ++c) bf[c] = 0.f;
-
+    // Two halves of 32 ratings; each issues its 8 row gathers before its MFMAs.
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      if (g * 16 < nrem) {  // wave-uniform: skip empty 16-rating groups
+    for (int h = 0; h < 2; ++h) {
+      if (h * 32 < nrem) {  // wave-uniform
+        float y[8][CN];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int t = 4 * g + j;
-          const float r = __shfl(rv, 4 * t + q);
-          float ym[CN], ya[CN];
-          float wb;
-#pragma unroll
-          for (int c = 0; c < CN; ++c) ym[c] = y[t][c] * dmask[c];
-          if constexpr (IMPLICIT) {
-            const float c1 = alpha * fabsf(r);
-            wb = r > 0.f ? 1.f + c1 : 0.f;
-#pragma unroll
-            for (int c = 0; c < CN; ++c) ya[c] = c1 * ym[c];
+        for (int t = 0; t < 8; ++t) {
+          const int src = 32 * h + 4 * t + q;
+          const int s = __shfl(ci, src);
+          if (src < nrem && dim_ok) {
+            load_dims<CN>(Y + (int64_t)s * ld + d0, y[t]);
           } else {
-            wb = r;
 #pragma unroll
-            for (int c = 0; c < CN; ++c) ya[c] = ym[c];
+            for (int c = 0; c < CN; ++c) y[t][c] = 0.f;
           }
-          int tt = 0;
+        }
 #pragma unroll
-          for (int c1 = 0; c1 < CN; ++c1) {
+        for (int g = 0; g < 2; ++g) {
+          if (32 * h + 16 * g < nrem) {  // wave-uniform: skip empty 16-rating groups
 #pragma unroll
-            for (int c2 = c1; c2 < CN; ++c2) {
-              acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c1], ym[c2], acc[tt], 0, 0, 0);
-              ++tt;
+            for (int j = 0; j < 4; ++j) {
+              const int t = 4 * g + j;
+              const float r = __shfl(rv, 32 * h + 4 * t + q);
+              float ym[CN], ya[CN];
+              float wb;
+#pragma unroll
+              for (int c = 0; c < CN; ++c) ym[c] = y[t][c] * dmask[c];
+              if constexpr (IMPLICIT) {
+                const float c1 = alpha * fabsf(r);
+                wb = r > 0.f ? 1.f + c1 : 0.f;
+#pragma unroll
+                for (int c = 0; c < CN; ++c) ya[c] = c1 * ym[c];
+              } else {
+                wb = r;
+#pragma unroll
+                for (int c = 0; c < CN; ++c) ya[c] = ym[c];
+              }
+              int tt = 0;
+#pragma unroll
+              for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+                for (int c2 = c1; c2 < CN; ++c2) {
+                  acc[tt] =
+                      __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c1], ym[c2], acc[tt], 0, 0, 0);
+                  ++tt;
+                }
+              }
+#pragma unroll
+              for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, ym[c], bf[c]);
             }
           }
-#pragma unroll
-          for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, ym[c], bf[c]);
         }
       }
     }
@@ -149,11 +154,21 @@ __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
   }
 }
 
-// Scatter the MFMA-layout Gram into the packed lower triangle in LDS.
+// (i, j) of register r of upper tile tt for this lane (MFMA 16x16 C layout:
+// row = 4q + r, col = m; dims interleaved as d = 16-index * CN + tile-index).
 template <int CN>
-__device__ __forceinline__ void pack_gram(const double (&a64)[Cfg<CN>::NT][4],
-                                          double* __restrict__ P) {
+__device__ __forceinline__ void tile_ij(int c1, int c2, int r, int& i, int& j) {
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  i = (4 * q + r) * CN + c1;
+  j = m * CN + c2;
+}
+
+// Complete the normal equations in fp64 registers (Spark CholeskySolver.solve:
+// ata[ii] += lambda * numExplicits; implicit: ls.merge(YtY)); padded dims get
+// an identity row so their solution is 0.
+template <int CN, bool IMPLICIT>
+__device__ __forceinline__ void regularise(double (&a64)[Cfg<CN>::NT][4], double lam, int k,
+                                           const double* __restrict__ yty) {
   int tt = 0;
 #pragma unroll
   for (int c1 = 0; c1 < CN; ++c1) {
@@ -161,98 +176,137 @@ __device__ __forceinline__ void pack_gram(const double (&a64)[Cfg<CN>::NT][4],
     for (int c2 = c1; c2 < CN; ++c2) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = (4 * q + r) * CN + c1, j = m * CN + c2;
-        const int hi = i > j ? i : j, lo = i > j ? j : i;
-        P[hi * (hi + 1) / 2 + lo] = a64[tt][r];
+        int i, j;
+        tile_ij<CN>(c1, c2, r, i, j);
+        if constexpr (IMPLICIT) {
+          const int hi = i > j ? i : j, lo = i > j ? j : i;
+          a64[tt][r] += yty[hi * (hi + 1) / 2 + lo];
+        }
+        if (c1 == c2 && i == j) a64[tt][r] = (i < k) ? a64[tt][r] + lam : 1.0;
       }
       ++tt;
     }
   }
 }
 
-// Row-per-lane fp64 Cholesky of the packed matrix P (KP x KP) with the rhs
-// (b[lane]) carried as an augmented column, then back substitution.  Writes
-// x to xrow[0..ld) (zero for dims >= k).  Returns false if a pivot <= 0.
-template <int KP>
-__device__ __forceinline__ bool chol_solve(double* __restrict__ P, double* __restrict__ cb,
-                                           double b, int k, float* __restrict__ xrow, int ld) {
+// Scatter the MFMA-layout matrix into the packed lower triangle P (type T) in LDS.
+template <int CN, class T>
+__device__ __forceinline__ void pack_gram(const double (&a64)[Cfg<CN>::NT][4], T* __restrict__ P) {
+  int tt = 0;
+#pragma unroll
+  for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+    for (int c2 = c1; c2 < CN; ++c2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int i, j;
+        tile_ij<CN>(c1, c2, r, i, j);
+        const int hi = i > j ? i : j, lo = i > j ? j : i;
+        P[hi * (hi + 1) / 2 + lo] = (T)a64[tt][r];
+      }
+      ++tt;
+    }
+  }
+}
+
+__device__ __forceinline__ float rcp_t(float d) { return __builtin_amdgcn_rcpf(d); }
+__device__ __forceinline__ double rcp_t(double d) {
+  double y = __builtin_amdgcn_rcp(d);  // v_rcp_f64 estimate + two Newton steps
+  y = fma(fma(-d, y, 1.0), y, y);
+  return fma(fma(-d, y, 1.0), y, y);
+}
+__device__ __forceinline__ float readlane_t(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ double readlane_t(double v, int l) { return readlane_f64(v, l); }
+
+// Row-per-lane LDL^T factorisation of the packed SPD matrix P (KP x KP, type T)
+// with the rhs (b[lane]) carried as an augmented column, then D^-1 and the
+// back substitution L^T x = z.  Mathematically the solve of Spark's dppsv
+// (Cholesky); the square-root-free form takes one reciprocal per pivot off
+// the dependency chain, and the pivot column is broadcast UNSCALED so its LDS
+// round trip overlaps that reciprocal.  T = float for explicit feedback (the
+// systems have cond ~ (lambda + |y|^2)/lambda; measured fp32 error ~1e-6 vs the
+// 1e-4 parity bar), T = double for implicit feedback (alpha-weighted systems
+// can be far worse conditioned).  One wavefront per workgroup, so
+// __syncthreads() is only an LDS wait plus a scheduling fence.
+template <int KP, class T>
+__device__ __forceinline__ bool ldl_solve(T* __restrict__ P, T* __restrict__ cb, T b, int k,
+                                          float* __restrict__ xrow, int ld) {
   const int lane = threadIdx.x & 63;
   const int rb = lane < KP ? lane * (lane + 1) / 2 : 0;
-  double a[KP];
+  T a[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) a[j] = P[rb + j];  // entries j > lane are never used
-  double mydinv = 0.0;
+  T myrd = T(0);
   bool ok = true;
 #pragma unroll
   for (int p = 0; p < KP; ++p) {
-    const double d = readlane_f64(a[p], p);
-    ok = ok && (d > 0.0);
-    const double dinv = 1.0 / sqrt(d);
-    const double l = a[p] * dinv;  // lane p: sqrt(d); lanes > p: L[lane][p]
-    if (lane >= p && lane < KP) P[rb + p] = l;  // final L, frees a[p]
-    if (lane == p) {
-      b *= dinv;
-      mydinv = dinv;
-    }
-    cb[lane] = l;
+    cb[lane] = a[p];                       // raw column p: A'[lane][p]
+    const T d = readlane_t(a[p], p);       // pivot D[p]
+    ok = ok && (d > T(0));
+    const T rd = rcp_t(d);
+    const T l = a[p] * rd;                 // L[lane][p] (lane p: 1)
+    a[p] = l;                              // row `lane` of L, written back after the loop
+    const T bp = readlane_t(b, p);         // z[p] * D[p] (forward elimination)
+    if (lane == p) myrd = rd;
+    if (lane > p) b -= l * bp;
     __syncthreads();
-    const double yp = readlane_f64(b, p);
 #pragma unroll
-    for (int j = p + 1; j < KP; ++j) a[j] = fma(-l, cb[j], a[j]);
-    if (lane > p) b = fma(-l, yp, b);
+    for (int j = p + 1; j < KP; ++j) a[j] -= l * cb[j];
     __syncthreads();
   }
-  // P now holds L (packed lower); solve L^T x = y by columns.
-  double x = 0.0;
+  // L (strict lower) back to P, z = D^-1 y, then L^T x = z by columns.
+#pragma unroll
+  for (int j = 0; j < KP; ++j)
+    if (j < lane && lane < KP) P[rb + j] = a[j];
+  __syncthreads();
+  b *= myrd;
+  T x = T(0);
 #pragma unroll
   for (int kk = KP - 1; kk >= 0; --kk) {
     const int off = kk * (kk + 1) / 2;
-    const double lk = lane < kk ? P[off + lane] : 0.0;
-    const double t = b * mydinv;
-    const double xk = readlane_f64(t, kk);
+    const T lk = lane < kk ? P[off + lane] : T(0);
+    const T xk = readlane_t(b, kk);
     if (lane == kk) x = xk;
-    b = fma(-lk, xk, b);
+    b -= lk * xk;
   }
-  if (!ok) x = 0.0;
+  if (!ok) x = T(0);
   for (int d = lane; d < ld; d += 64) xrow[d] = (d < k) ? (float)x : 0.f;
   return ok;
 }
 
-// Shared tail: cross-slot rhs reduce, pack, regularise, solve.
+template <bool IMPLICIT>
+struct SolvePrec { typedef float T; };
+template <>
+struct SolvePrec<true> { typedef double T; };
+
+// Shared tail: cross-slot rhs reduce, regularise, pack, solve.
 template <int CN, bool IMPLICIT>
 __device__ __forceinline__ void finish_and_solve(double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
-                                                 int64_t n_reg, double* __restrict__ P,
-                                                 double* __restrict__ cb, int k, float reg,
-                                                 const double* __restrict__ yty,
+                                                 int64_t n_reg, typename SolvePrec<IMPLICIT>::T* P,
+                                                 typename SolvePrec<IMPLICIT>::T* cb, int k,
+                                                 float reg, const double* __restrict__ yty,
                                                  float* __restrict__ xrow, int ld, int row,
                                                  int32_t* __restrict__ status) {
-  constexpr int KP = Cfg<CN>::KP, NP = Cfg<CN>::NP;
+  typedef typename SolvePrec<IMPLICIT>::T T;
+  constexpr int KP = Cfg<CN>::KP;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
 #pragma unroll
   for (int c = 0; c < CN; ++c) {
     b64[c] += shfl_xor_f64(b64[c], 16);
     b64[c] += shfl_xor_f64(b64[c], 32);
   }
-  pack_gram<CN>(a64, P);
+  regularise<CN, IMPLICIT>(a64, (double)reg * (double)n_reg, k, yty);
+  pack_gram<CN, T>(a64, P);
   if (q == 0) {
 #pragma unroll
-    for (int c = 0; c < CN; ++c) cb[m * CN + c] = b64[c];
+    for (int c = 0; c < CN; ++c) cb[m * CN + c] = (T)b64[c];
   }
   __syncthreads();
-  if constexpr (IMPLICIT) {
-    for (int e = lane; e < NP; e += 64) P[e] += yty[e];
-    __syncthreads();
-  }
-  if (lane < KP) {
-    const int di = lane * (lane + 1) / 2 + lane;
-    if (lane < k)
-      P[di] += (double)reg * (double)n_reg;
-    else
-      P[di] = 1.0;  // padded dims: identity rows, rhs 0 -> x = 0
-  }
-  const double b = lane < KP ? cb[lane] : 0.0;
+  const T b = lane < KP ? cb[lane] : T(0);
   __syncthreads();
-  const bool ok = chol_solve<KP>(P, cb, b, k, xrow, ld);
+  const bool ok = ldl_solve<KP, T>(P, cb, b, k, xrow, ld);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -297,8 +351,9 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
-  __shared__ double P[Cfg<CN>::NP];
-  __shared__ double cb[64];
+  typedef typename SolvePrec<IMPLICIT>::T T;
+  __shared__ T P[Cfg<CN>::NP];
+  __shared__ T cb[64];
   const int task = blockIdx.x;
   double a64[NT][4];
 #pragma unroll
@@ -331,8 +386,9 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
-  __shared__ double P[Cfg<CN>::NP];
-  __shared__ double cb[64];
+  typedef typename SolvePrec<IMPLICIT>::T T;
+  __shared__ T P[Cfg<CN>::NP];
+  __shared__ T cb[64];
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
   double a64[NT][4];
@@ -387,7 +443,7 @@ __global__ __launch_bounds__(64) void yty_reduce_kernel(const double* __restrict
   for (int c = 0; c < CN; ++c) b64[c] = 0.0;
   int npos = 0;
   for (int s = 0; s < nslots; ++s) add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
-  pack_gram<CN>(a64, P);
+  pack_gram<CN, double>(a64, P);
   __syncthreads();
   for (int e = threadIdx.x; e < NP; e += 64) out[e] = P[e];
 }
@@ -412,7 +468,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int64_t* chunk_begin, const int64_t* chunk_end, int32_t n_chunks,
                    const float* Y_src, float* X_dst, int32_t ld, int32_t k, float reg,
                    int implicit, float alpha, const double* yty_packed, int32_t* status_dev,
-                   void* ws, size_t ws_bytes, void* stream) {
+                   void* ws, size_t ws_bytes, int phases, void* stream) {
   ALS_REQUIRE(k >= 1 && k <= 64, ALS_EUNSUPPORTED, "als_solve_half: rank %d not in [1, 64]", k);
   ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_solve_half: ld=%d must be >= k and %%4==0",
               ld);
@@ -429,8 +485,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   hipStream_t st = as_stream(stream);
   double* slots = static_cast<double*>(ws);
   const int cn = cn_for_k(k);
-  const unsigned g1 = (unsigned)(n_chunks + n_light);
-  const unsigned g2 = (unsigned)n_heavy;
+  ALS_REQUIRE(phases >= 1 && phases <= 3, ALS_EINVAL, "als_solve_half: phases must be 1, 2 or 3");
+  const unsigned g1 = (phases & 1) ? (unsigned)(n_chunks + n_light) : 0u;
+  const unsigned g2 = (phases & 2) ? (unsigned)n_heavy : 0u;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
     if (g1)                                                                                       \

@@ -163,8 +163,9 @@ def compute_yty(Y: torch.Tensor, n: int, rank: int, ws: Workspace) -> torch.Tens
 
 def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, reg: float,
                implicit: bool, alpha: float, yty: Optional[torch.Tensor],
-               status: torch.Tensor, ws: Workspace) -> None:
-    """One computeFactors pass: X[row] <- solve(A_row, b_row) for every row of `block`."""
+               status: torch.Tensor, ws: Workspace, phases: int = 3) -> None:
+    """One computeFactors pass: X[row] <- solve(A_row, b_row) for every row of `block`.
+    phases: 1 = launch 1 only, 2 = launch 2 only, 3 = both (see als_hip.h)."""
     L = _lib.lib()
     w = ws.get(L.als_solve_workspace_bytes(rank, block.n_chunks))
     check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
@@ -172,7 +173,7 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
                            ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),
                            ptr(block.chunk_begin), ptr(block.chunk_end), block.n_chunks,
                            ptr(Y), ptr(X), X.shape[1], rank, float(reg), int(bool(implicit)),
-                           float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(),
+                           float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(), int(phases),
                            stream_ptr(X.device)), "als_solve_half")
 
 

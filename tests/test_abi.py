@@ -1,0 +1,110 @@
+"""CPU tests of the drop-in boundary (no GPU needed, no compute launched).
+
+* libals_hip.so loads and exports every function declared in include/als_hip.h.
+* The ctypes signature table in _lib.py covers exactly those symbols.
+* Workspace-size functions and argument validation run host-side and return
+  the documented error codes before touching a device.
+* The product fails loudly (no CPU fallback) when no GPU is visible.
+"""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import als_mi355x
+from als_mi355x import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "als_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*[a-z_0-9 ]+\**\s*\**\b(als_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_abi():
+    names = declared_functions()
+    for must in ["als_solve_half", "als_csr_build", "als_index_build", "als_yty", "als_predict",
+                 "als_rmse_partial", "als_topk", "als_schedule_build", "als_last_error"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(raw, name), f"{name} declared in als_hip.h but not exported"
+    assert sorted(_lib.SIGNATURES) == declared_functions()
+    assert L.als_abi_version() == _lib.ABI_VERSION
+
+
+def test_abi_version_macro_matches():
+    m = re.search(r"#define ALS_ABI_VERSION (\d+)", open(HEADER).read())
+    assert int(m.group(1)) == _lib.ABI_VERSION
+
+
+def test_workspace_sizes_are_monotone_and_host_only():
+    L = _lib.lib()
+    assert L.als_csr_workspace_bytes(1000, 10) < L.als_csr_workspace_bytes(10 ** 7, 10 ** 5)
+    assert L.als_index_workspace_bytes(10, 100) < L.als_index_workspace_bytes(10, 10 ** 6)
+    assert L.als_solve_workspace_bytes(64, 0) < L.als_solve_workspace_bytes(64, 100)
+    assert L.als_solve_workspace_bytes(10, 100) < L.als_solve_workspace_bytes(64, 100)
+    assert L.als_yty_workspace_bytes(10 ** 6, 64) > 0
+    assert L.als_rmse_workspace_bytes(10 ** 6) > L.als_rmse_workspace_bytes(10)
+    assert [L.als_k_pad(k) for k in (1, 16, 17, 32, 33, 64)] == [16, 16, 32, 32, 64, 64]
+
+
+def _solve_args(**over):
+    a = dict(row_ptr=1, col=1, val=1, light=1, n_light=1, heavy=1, slot=1, n_heavy=0, crow=1,
+             cbeg=1, cend=1, n_chunks=0, Y=16, X=16, ld=64, k=64, reg=0.1, implicit=0, alpha=1.0,
+             yty=0, status=1, ws=1, ws_bytes=1 << 20, phases=3, stream=0)
+    a.update(over)
+    return list(a.values())
+
+
+@pytest.mark.parametrize("over,code", [
+    (dict(k=0), -4), (dict(k=65), -4), (dict(ld=62), -1), (dict(ld=32), -1),
+    (dict(n_light=-1), -1), (dict(Y=0), -1), (dict(implicit=1), -1), (dict(reg=-1.0), -1),
+    (dict(Y=18), -1), (dict(phases=0), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2)])
+def test_solve_half_argument_errors(over, code):
+    L = _lib.lib()
+    rc = L.als_solve_half(*_solve_args(**over))
+    assert rc == code
+    assert L.als_last_error()  # a message is set
+
+
+def test_topk_and_predict_argument_errors():
+    L = _lib.lib()
+    assert L.als_topk(1, 1, 1, 1, 64, 64, 0, 1, 1, 0, 0, 0) == -4      # top = 0
+    assert L.als_topk(1, 1, 1, 1, 64, 64, 257, 1, 1, 0, 0, 0) == -4    # top > 256
+    assert L.als_topk(1, 1, 1, 1, 60, 64, 10, 1, 1, 0, 0, 0) == -1     # ld < k
+    assert L.als_predict(1, 1, 5, 1, 1, 1, 1, 1, 1, 10, 0, 1, 0) == -1  # k = 0
+    assert L.als_csr_build(0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0) == -1
+    assert L.als_index_build(0, 0, 0, 0, 0, 0, 0, 0, 0) == -1           # id_space 0
+
+
+def test_zero_size_calls_are_noops():
+    L = _lib.lib()
+    assert L.als_predict(0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4, 0, 0) == 0
+    assert L.als_topk(0, 0, 0, 0, 4, 4, 1, 0, 0, 0, 0, 0) == 0
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_product_refuses_to_run_without_gpu():
+    from als_mi355x.engine import ALSCore
+    with pytest.raises(_lib.ALSNativeError, match="no CPU fallback"):
+        ALSCore([0, 1], [0, 1], [1.0, 2.0])
+
+
+def test_product_never_imports_the_oracle():
+    pkg = os.path.dirname(als_mi355x.__file__)
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in re.sub(r'""".*?"""|#.*', "", src, flags=re.S), f

@@ -1,0 +1,83 @@
+"""Fold rocprofv3 outputs of tools/profile.sh into profiles/:
+  profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats summary, copied)
+  profiles/<tag>_pmc.json           (per-kernel FETCH_SIZE / WRITE_SIZE per launch)
+  profiles/pmc_summary.json         (what bench.py reads for roofline.traffic)
+
+gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports 1/2 of the
+bytes of wide (16 B/lane) coalesced reads; the dominant kernel's factor-row
+gathers are 16 B/lane float4 loads, so fetch bytes are doubled.  WRITE_SIZE is
+exact for 16-B stores.  Infinity-Cache hits are counted by these counters.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+out_dir, tag = sys.argv[1], sys.argv[2]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+prof = os.path.join(ROOT, "profiles")
+os.makedirs(prof, exist_ok=True)
+
+
+def find(pattern):
+    hits = sorted(glob.glob(os.path.join(out_dir, "**", pattern), recursive=True))
+    return hits[0] if hits else None
+
+
+stats = find("*kernel_stats.csv")
+if stats:
+    shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
+
+
+def short(name):
+    name = name.split("(")[0]
+    for k in ("gram_solve_kernel", "reduce_solve_kernel", "topk_kernel", "yty_partial_kernel",
+              "rs_scatter_kernel", "predict_kernel", "rmse_partial_kernel"):
+        if k in name:
+            return k
+    return name[-60:]
+
+
+def counters(path, counter):
+    per = defaultdict(list)
+    if not path:
+        return per
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            per[(short(row["Kernel_Name"]), row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return per
+
+
+fetch = counters(find("pmc_fetch/**/*counter_collection.csv") or
+                 find("*pmc_fetch*counter_collection.csv"), "FETCH_SIZE")
+write = counters(find("pmc_write/**/*counter_collection.csv") or
+                 find("*pmc_write*counter_collection.csv"), "WRITE_SIZE")
+summary = {}
+for key in set(fetch) | set(write):
+    s, full = key
+    f = fetch.get(key, [])
+    w = write.get(key, [])
+    fk = sum(f) / len(f) if f else None  # KiB per dispatch
+    wk = sum(w) / len(w) if w else None
+    ent = summary.setdefault(s, {"dispatch_variants": []})
+    ent["dispatch_variants"].append({
+        "kernel": full[:200], "dispatches": max(len(f), len(w)),
+        "fetch_kib_raw": fk, "write_kib": wk})
+for s, ent in summary.items():
+    tot_f = sum((v["fetch_kib_raw"] or 0) * v["dispatches"] for v in ent["dispatch_variants"])
+    tot_w = sum((v["write_kib"] or 0) * v["dispatches"] for v in ent["dispatch_variants"])
+    n = sum(v["dispatches"] for v in ent["dispatch_variants"])
+    ent["fetch_bytes_per_launch_raw"] = 1024 * tot_f / n
+    ent["fetch_bytes_per_launch_corrected_x2"] = 2 * 1024 * tot_f / n
+    ent["write_bytes_per_launch"] = 1024 * tot_w / n
+    ent["hbm_bytes_per_launch"] = ent["fetch_bytes_per_launch_corrected_x2"] + ent["write_bytes_per_launch"]
+with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as fh:
+    json.dump(summary, fh, indent=1)
+with open(os.path.join(prof, "pmc_summary.json"), "w") as fh:
+    json.dump({"source": f"profiles/{tag}_pmc.json", **summary}, fh, indent=1)
+print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in summary.items()}))

@@ -276,21 +276,277 @@ __device__ __forceinline__ bool ldl_solve(T* __restrict__ P, T* __restrict__ cb,
   return ok;
 }
 
+// Panel-blocked form of ldl_solve (same arithmetic, PW = 4 columns per panel):
+// inside a panel each pivot and each in-panel update use scalar broadcasts
+// (v_readlane) only; the trailing update of the remaining columns is one LDS
+// round trip per panel (each lane publishes its 4 unscaled panel entries as one
+// 16-byte record, every lane streams the records of rows j > panel with
+// broadcast ds_read_b128 and applies 4 FMAs per record).  16 LDS round trips
+// instead of 64 on the pivot chain.
+template <int KP, class T>
+__device__ __forceinline__ bool ldl_blocked(T* __restrict__ P, T* __restrict__ cb, T b, int k,
+                                            float* __restrict__ xrow, int ld) {
+  constexpr int PW = 4;
+  static_assert(KP % PW == 0, "KP must be a multiple of the panel width");
+  const int lane = threadIdx.x & 63;
+  const int rb = lane < KP ? lane * (lane + 1) / 2 : 0;
+  T a[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) a[j] = P[rb + j];  // entries j > lane are never used
+  T myrd = T(0);
+  bool ok = true;
+#pragma unroll
+  for (int pb = 0; pb < KP; pb += PW) {
+    T l[PW], u[PW];
+#pragma unroll
+    for (int c = 0; c < PW; ++c) {
+      const int p = pb + c;
+      u[c] = a[p];                         // A'[lane][p] before elimination of p
+      const T d = readlane_t(a[p], p);     // pivot D[p]
+      ok = ok && (d > T(0));
+      const T rd = rcp_t(d);
+      l[c] = u[c] * rd;                    // L[lane][p]
+      a[p] = l[c];
+      if (lane == p) myrd = rd;
+      const T bp = readlane_t(b, p);
+      if (lane > p) b -= l[c] * bp;
+#pragma unroll
+      for (int c2 = c + 1; c2 < PW; ++c2) a[pb + c2] -= l[c] * readlane_t(u[c], pb + c2);
+    }
+    if (pb + PW < KP) {
+#pragma unroll
+      for (int c = 0; c < PW; ++c) cb[PW * lane + c] = u[c];
+      __syncthreads();  // 1-wave workgroup: an LDS wait + scheduling fence only
+#pragma unroll
+      for (int j = pb + PW; j < KP; ++j) {
+#pragma unroll
+        for (int c = 0; c < PW; ++c) a[j] -= l[c] * cb[PW * j + c];
+      }
+      __syncthreads();
+    }
+  }
+  // L (strict lower) to P, z = D^-1 y, then L^T x = z by columns.
+#pragma unroll
+  for (int j = 0; j < KP; ++j)
+    if (j < lane && lane < KP) P[rb + j] = a[j];
+  __syncthreads();
+  b *= myrd;
+  T x = T(0);
+#pragma unroll
+  for (int kk = KP - 1; kk >= 0; --kk) {
+    const int off = kk * (kk + 1) / 2;
+    const T lk = lane < kk ? P[off + lane] : T(0);
+    const T xk = readlane_t(b, kk);
+    if (lane == kk) x = xk;
+    b -= lk * xk;
+  }
+  if (!ok) x = T(0);
+  for (int d = lane; d < ld; d += 64) xrow[d] = (d < k) ? (float)x : 0.f;
+  return ok;
+}
+
+// ---------------------------------------------------------------------------
+// Block LDL^T on the matrix cores (explicit path).
+//
+// The regularised Gram arrives as fp32 16x16 tiles in the MFMA C layout
+// (A[t] = tile (I, J), I <= J; dims permuted so that block I holds the dims
+// d = 16-index * CN + I).  Any symmetric permutation is a valid pivot order, so
+// the matrix is factored as A = U^T D U (U unit upper) in that block order:
+//   for K: factor B_KK = U_KK^T D_K U_KK              (16x16, row-per-lane, 16 lanes)
+//          W_KJ = U_KK^-T B_KJ, U_KJ = D_K^-1 W_KJ     (TRSM, one lane per column)
+//          B_IJ -= U_KI^T W_KJ   for K < I <= J        (v_mfma_f32_16x16x4_f32, 4 per tile)
+// The rhs rides along as one more TRSM column (forward substitution), then a
+// block back substitution finishes x.  The O(k^3) trailing work runs on the
+// MFMA pipe; the VALU keeps only the 16-wide diagonal factorisations and TRSMs.
+// LDS (floats): U tiles NT*256 (diagonal slots hold L_K rows) | stage/W NB*320 |
+// D, b, z, x 4*16*NB.
+// ---------------------------------------------------------------------------
+template <int CN>
+struct TileLds {
+  static constexpr int NB = CN, NT = CN * (CN + 1) / 2;
+  static constexpr int U = 0, S = NT * 256, D = S + NB * 320, B = D + 16 * NB,
+                       Z = B + 16 * NB, X = Z + 16 * NB, SIZE = X + 16 * NB;
+};
+
+__host__ __device__ constexpr int tile_index(int nb, int i, int j) {
+  // upper tiles in (c1, c2 >= c1) row order, as the Gram accumulates them
+  return i * nb - i * (i - 1) / 2 + (j - i);
+}
+
+template <int CN>
+__device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const double (&b64)[CN],
+                                               float* __restrict__ lds, int k,
+                                               float* __restrict__ xrow, int ld) {
+  typedef TileLds<CN> Lo;
+  constexpr int NB = CN;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  float* Ust = lds + Lo::U;
+  float* St = lds + Lo::S;
+  float* Dv = lds + Lo::D;
+  float* bv = lds + Lo::B;
+  float* zv = lds + Lo::Z;
+  float* xv = lds + Lo::X;
+  if (q == 0) {
+#pragma unroll
+    for (int c = 0; c < CN; ++c) bv[c * 16 + m] = (float)b64[c];
+  }
+  bool ok = true;
+#pragma unroll
+  for (int K = 0; K < NB; ++K) {
+    // (a) stage block row K transposed: St[J-K][j][k] (row stride 20 floats)
+#pragma unroll
+    for (int J = K; J < NB; ++J) {
+      const floatx4 v = A[tile_index(NB, K, J)];
+      *reinterpret_cast<float4*>(St + (J - K) * 320 + m * 20 + 4 * q) =
+          make_float4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+    // (b) LDL^T of the diagonal block, row `i` per lane (lanes >= 16 mirror lanes 0..15).
+    //     Broadcasts are v_readlane (no LDS round trip on the 16-step pivot chain).
+    const int i = lane & 15;
+    float a[16];
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const float4 v = *reinterpret_cast<const float4*>(St + i * 20 + 4 * c4);
+      a[4 * c4] = v.x; a[4 * c4 + 1] = v.y; a[4 * c4 + 2] = v.z; a[4 * c4 + 3] = v.w;
+    }
+    float myd = 1.f;
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const float d = readlane_t(a[p], p);
+      ok = ok && (d > 0.f);
+      float u[16];
+#pragma unroll
+      for (int j = p + 1; j < 16; ++j) u[j] = readlane_t(a[p], j);  // A'[j][p]
+      const float l = a[p] * rcp_t(d);                                 // L[i][p]
+#pragma unroll
+      for (int j = p + 1; j < 16; ++j) a[j] = fmaf(-l, u[j], a[j]);
+      a[p] = l;
+      if (i == p) myd = d;
+    }
+    float* Lk = Ust + 256 * tile_index(NB, K, K);  // row-major L_K rows (for the back solve)
+    if (lane < 16) {
+      Dv[K * 16 + i] = myd;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        *reinterpret_cast<float4*>(Lk + i * 16 + 4 * c4) =
+            make_float4(a[4 * c4], a[4 * c4 + 1], a[4 * c4 + 2], a[4 * c4 + 3]);
+    }
+    // (c) TRSM: lane t < 16*(NB-1-K) owns column (t&15) of block J = K+1+(t>>4);
+    //     lane 16*(NB-1-K) owns the rhs block b_K.  L[p][c] comes from lane p by readlane.
+    const int ncol = 16 * (NB - 1 - K);
+    const int Jl = K + 1 + (lane >> 4);
+    const bool is_col = lane < ncol, is_rhs = lane == ncol;
+    float w[16];
+    {
+      const float* src = is_col ? St + (Jl - K) * 320 + (lane & 15) * 20 : bv + K * 16;
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
+        w[4 * c4] = v.x; w[4 * c4 + 1] = v.y; w[4 * c4 + 2] = v.z; w[4 * c4 + 3] = v.w;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+#pragma unroll
+      for (int p = c + 1; p < 16; ++p) w[p] = fmaf(-readlane_t(a[c], p), w[c], w[p]);
+    }
+    __syncthreads();  // all stage reads done before W overwrites the stage
+    if (is_col) {
+      float* Wd = St + (Jl - K - 1) * 256 + (lane & 15);
+      float* Ud = Ust + 256 * tile_index(NB, K, Jl) + (lane & 15);
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        Wd[c * 16] = w[c];
+        Ud[c * 16] = w[c] * rcp_t(readlane_t(myd, c));
+      }
+    } else if (is_rhs) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        *reinterpret_cast<float4*>(zv + K * 16 + 4 * c4) =
+            make_float4(w[4 * c4], w[4 * c4 + 1], w[4 * c4 + 2], w[4 * c4 + 3]);
+    }
+    __syncthreads();
+    // (d) trailing update on the matrix cores + rhs update b_J -= U_KJ^T z_K
+#pragma unroll
+    for (int I = K + 1; I < NB; ++I) {
+      float ua[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) ua[s4] = -Ust[256 * tile_index(NB, K, I) + (4 * s4 + q) * 16 + m];
+#pragma unroll
+      for (int J = I; J < NB; ++J) {
+        floatx4 acc = A[tile_index(NB, I, J)];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              ua[s4], St[(J - K - 1) * 256 + (4 * s4 + q) * 16 + m], acc, 0, 0, 0);
+        A[tile_index(NB, I, J)] = acc;
+      }
+    }
+    if (is_col) {
+      const float* Uc = Ust + 256 * tile_index(NB, K, Jl) + (lane & 15);
+      float t = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) t = fmaf(Uc[c * 16], zv[K * 16 + c], t);
+      bv[Jl * 16 + (lane & 15)] -= t;
+    }
+    __syncthreads();
+  }
+  // (e) block back substitution: x_K = U_KK^-1 (D_K^-1 z_K - sum_{J>K} U_KJ x_J)
+#pragma unroll
+  for (int K = NB - 1; K >= 0; --K) {
+    const int i = lane & 15;
+    float v = zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
+#pragma unroll
+    for (int J = K + 1; J < NB; ++J) {
+      const float* Ur = Ust + 256 * tile_index(NB, K, J) + i * 16;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v = fmaf(-Ur[j], xv[J * 16 + j], v);
+    }
+    const float* Lk = Ust + 256 * tile_index(NB, K, K) + i;
+    float ur[16];  // ur[j] = U_KK[i][j] = L_K[j][i]
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ur[j] = Lk[j * 16];
+    float x = 0.f;
+#pragma unroll
+    for (int j = 15; j >= 0; --j) {
+      const float xj = readlane_t(v, j);
+      if (i == j) x = xj;
+      if (i < j) v = fmaf(-ur[j], xj, v);
+    }
+    if (lane < 16) xv[K * 16 + i] = x;
+    __syncthreads();
+  }
+  // (f) un-permute: dim d = i*CN + K  <->  xv[K*16 + i]
+  for (int d = lane; d < ld; d += 64) {
+    const float x = d < 16 * CN ? xv[(d % CN) * 16 + d / CN] : 0.f;
+    xrow[d] = (d < k && ok) ? x : 0.f;
+  }
+  return ok;
+}
+
 template <bool IMPLICIT>
 struct SolvePrec { typedef float T; };
 template <>
 struct SolvePrec<true> { typedef double T; };
 
-// Shared tail: cross-slot rhs reduce, regularise, pack, solve.
+template <int CN, bool IMPLICIT>
+struct SmemBytes {
+  static constexpr int value = IMPLICIT
+      ? (int)sizeof(double) * (Cfg<CN>::NP + 64 * 4)
+      : (int)sizeof(float) * TileLds<CN>::SIZE;
+};
+
+// Shared tail: cross-slot rhs reduce, regularise (fp64), then
+//   explicit: fp32 tiles -> block LDL^T on the matrix cores (tile_ldl_solve)
+//   implicit: fp64 packed rows -> row-per-lane LDL^T (ldl_blocked<double>)
 template <int CN, bool IMPLICIT>
 __device__ __forceinline__ void finish_and_solve(double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
-                                                 int64_t n_reg, typename SolvePrec<IMPLICIT>::T* P,
-                                                 typename SolvePrec<IMPLICIT>::T* cb, int k,
+                                                 int64_t n_reg, unsigned char* smem, int k,
                                                  float reg, const double* __restrict__ yty,
                                                  float* __restrict__ xrow, int ld, int row,
                                                  int32_t* __restrict__ status) {
-  typedef typename SolvePrec<IMPLICIT>::T T;
-  constexpr int KP = Cfg<CN>::KP;
+  constexpr int KP = Cfg<CN>::KP, NT = Cfg<CN>::NT;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
 #pragma unroll
   for (int c = 0; c < CN; ++c) {
@@ -298,15 +554,27 @@ __device__ __forceinline__ void finish_and_solve(double (&a64)[Cfg<CN>::NT][4], 
     b64[c] += shfl_xor_f64(b64[c], 32);
   }
   regularise<CN, IMPLICIT>(a64, (double)reg * (double)n_reg, k, yty);
-  pack_gram<CN, T>(a64, P);
-  if (q == 0) {
+  bool ok;
+  if constexpr (!IMPLICIT) {
+    floatx4 A[NT];
 #pragma unroll
-    for (int c = 0; c < CN; ++c) cb[m * CN + c] = (T)b64[c];
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[t][r] = (float)a64[t][r];
+    ok = tile_ldl_solve<CN>(A, b64, reinterpret_cast<float*>(smem), k, xrow, ld);
+  } else {
+    double* P = reinterpret_cast<double*>(smem);
+    double* cb = P + Cfg<CN>::NP;
+    pack_gram<CN, double>(a64, P);
+    if (q == 0) {
+#pragma unroll
+      for (int c = 0; c < CN; ++c) cb[m * CN + c] = b64[c];
+    }
+    __syncthreads();
+    const double b = lane < KP ? cb[lane] : 0.0;
+    __syncthreads();
+    ok = ldl_blocked<KP, double>(P, cb, b, k, xrow, ld);
   }
-  __syncthreads();
-  const T b = lane < KP ? cb[lane] : T(0);
-  __syncthreads();
-  const bool ok = ldl_solve<KP, T>(P, cb, b, k, xrow, ld);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -351,9 +619,7 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
-  typedef typename SolvePrec<IMPLICIT>::T T;
-  __shared__ T P[Cfg<CN>::NP];
-  __shared__ T cb[64];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
   const int task = blockIdx.x;
   double a64[NT][4];
 #pragma unroll
@@ -374,7 +640,7 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
   const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
   gram_accumulate<CN, IMPLICIT, false>(col, val, pb, pe, Y, ld, k, alpha, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, P, cb, k, reg, yty, X + (int64_t)row * ld, ld,
+  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, smem, k, reg, yty, X + (int64_t)row * ld, ld,
                                  row, status);
 }
 
@@ -386,9 +652,7 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
-  typedef typename SolvePrec<IMPLICIT>::T T;
-  __shared__ T P[Cfg<CN>::NP];
-  __shared__ T cb[64];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
   double a64[NT][4];
@@ -403,7 +667,7 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
     add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
-  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, P, cb, k, reg, yty, X + (int64_t)row * ld, ld,
+  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, smem, k, reg, yty, X + (int64_t)row * ld, ld,
                                  row, status);
 }
 

@@ -1,0 +1,67 @@
+"""Dev tool: time the phases of the light-row half-sweep kernel on the ML-25M-shaped
+synthetic data (see tools/dev_ablate.hip).  Run on the GPU box:
+    python tools/ablate.py
+Prints ms per launch for each mode on the item side and the user side."""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+from als_mi355x import datasets as D, engine as E  # noqa: E402
+
+SO = os.path.join(ROOT, "tools", "libals_dev.so")
+
+
+def build():
+    src = os.path.join(ROOT, "tools", "dev_ablate.hip")
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-shared", "--offload-arch=gfx950",
+                           "-std=c++17", src, "-o", SO])
+
+
+def main():
+    if "--build" in sys.argv:
+        build()
+        return
+    L = ctypes.CDLL(SO)
+    P = ctypes.c_void_p
+    L.dev_ablate.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int,
+                             ctypes.c_float, P, P]
+    dev = torch.device("cuda", 0)
+    u, i, r = D.synthetic_config("ml25m", device=dev)
+    core = E.ALSCore(u, i, r, device=dev)
+    core.init_factors(64, seed=5)
+    core.iterate(0.1)
+    torch.cuda.synchronize()
+    st = torch.zeros(1, dtype=torch.int32, device=dev)
+    names = {0: "full (tile LDL)", 1: "gram only", 2: "solve only (tile LDL)",
+             3: "solve only (unblocked)", 4: "full (unblocked LDL)",
+             5: "half gram / half solve"}
+    for side, blk, Y, X in (("item", core.item_block, core.U, core.V),
+                            ("user", core.user_block, core.V, core.U)):
+        X2 = torch.empty_like(X)
+        for mode in (0, 1, 2, 3, 4, 5):
+            times = []
+            for rep in range(4):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                rc = L.dev_ablate(mode, blk.row_ptr.data_ptr(), blk.col.data_ptr(),
+                                  blk.val.data_ptr(), blk.light_rows.data_ptr(), blk.n_light,
+                                  Y.data_ptr(), X2.data_ptr(), 64, 0.1, st.data_ptr(),
+                                  torch.cuda.current_stream().cuda_stream)
+                e1.record()
+                torch.cuda.synchronize()
+                assert rc == 0
+                times.append(e0.elapsed_time(e1))
+            t = sorted(times[1:])[1]
+            print(f"{side:5s} rows={blk.n_light:7d} mode {mode} {names[mode]:24s} {t:8.3f} ms"
+                  f"  {1e6 * t / blk.n_light:8.2f} ns/row", flush=True)
+
+
+if __name__ == "__main__":
+    main()

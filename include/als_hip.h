@@ -18,7 +18,8 @@
  *    All compute calls are asynchronous on that stream.
  *  - Factor matrices are row-major fp32 with leading dimension `ld`
  *    (ld % 4 == 0, ld >= k, base 16-byte aligned).  Output factor rows are
- *    written in full: columns [k, ld) are written as zero.
+ *    written in full: columns [k, ld) are written as zero, and factor inputs
+ *    (Y_src of als_solve_half / als_yty) must carry zeros there too.
  *  - Return value: 0 on success, negative ALS_E* code on argument error;
  *    als_last_error() returns a thread-local message for the last failure.
  *  - Dense indices: ids are mapped to dense row numbers in ascending id order

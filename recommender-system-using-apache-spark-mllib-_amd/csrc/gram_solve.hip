@@ -56,101 +56,128 @@ __device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y
   }
 }
 
+// Gather the factor rows of one half-block (32 ratings = 8 MFMA steps) into
+// registers: step t, lane (q, m) gets dims m*CN .. m*CN+CN-1 of rating 4t+q.
+template <int CN>
+__device__ __forceinline__ void gather_half(float (&y)[8][CN], int ci, int base, int nrem,
+                                            const float* __restrict__ Y, int ld, int d0,
+                                            bool dim_ok) {
+  const int q = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int src = base + 4 * t + q;
+    const int s = __shfl(ci, src);
+    if (src < nrem && dim_ok) {
+      load_dims<CN>(Y + (int64_t)s * ld + d0, y[t]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < CN; ++c) y[t][c] = 0.f;
+    }
+  }
+}
+
+// MFMA over one gathered half-block: acc[tile] += (w_a y)(y)^T, bf += w_b y.
+template <int CN, bool IMPLICIT>
+__device__ __forceinline__ void mfma_half(const float (&y)[8][CN], float rv, int base, int nrem,
+                                          float alpha, floatx4 (&acc)[Cfg<CN>::NT],
+                                          float (&bf)[CN]) {
+  const int q = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if (base + 16 * g < nrem) {  // wave-uniform: skip empty 16-rating groups
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int t = 4 * g + j;
+        const float r = __shfl(rv, base + 4 * t + q);
+        float ym[CN], ya[CN];
+        float wb;
+#pragma unroll
+        for (int c = 0; c < CN; ++c) ym[c] = y[t][c];
+        if constexpr (IMPLICIT) {
+          const float c1 = alpha * fabsf(r);
+          wb = r > 0.f ? 1.f + c1 : 0.f;
+#pragma unroll
+          for (int c = 0; c < CN; ++c) ya[c] = c1 * ym[c];
+        } else {
+          wb = r;
+#pragma unroll
+          for (int c = 0; c < CN; ++c) ya[c] = ym[c];
+        }
+        int tt = 0;
+#pragma unroll
+        for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+          for (int c2 = c1; c2 < CN; ++c2) {
+            acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c1], ym[c2], acc[tt], 0, 0, 0);
+            ++tt;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, ym[c], bf[c]);
+      }
+    }
+  }
+}
+
 // Accumulate the (weighted) Gram and rhs of ratings [pb, pe) of one row.
-// a64[t][r]: lane's 4 accumulator rows of upper tile t (MFMA C layout);
-// b64[c]: this lane's partial rhs for dim m*CN+c over its rating slot q
-// (summed over q by the caller).  npos: #ratings > 0 (implicit only).
-template <int CN, bool IMPLICIT, bool IDENT>
+// tot[t][r]: this lane's 4 accumulator rows of upper tile t (MFMA C layout),
+// summed over 64-rating blocks in AccT (each block's own sum is an exact-product
+// fp32 MFMA chain of <= 16 steps); btot[c]: partial rhs for dim m*CN+c over this
+// lane's rating slot q (summed over q by the caller); npos: #ratings > 0.
+// Software pipeline: the row gathers of half-block h+1 are in flight while the
+// MFMAs of half-block h run; rating indices are loaded one 64-block ahead.
+template <int CN, bool IMPLICIT, bool IDENT, class AccT>
 __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
                                                 const float* __restrict__ val, int64_t pb,
                                                 int64_t pe, const float* __restrict__ Y, int ld,
                                                 int k, float alpha,
-                                                double (&a64)[Cfg<CN>::NT][4],
-                                                double (&b64)[CN], int& npos) {
+                                                AccT (&tot)[Cfg<CN>::NT][4], AccT (&btot)[CN],
+                                                int& npos) {
   constexpr int NT = Cfg<CN>::NT;
-  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int lane = threadIdx.x & 63, m = lane & 15;
   const int d0 = m * CN;
-  const bool dim_ok = d0 < k;
-  float dmask[CN];
-#pragma unroll
-  for (int c = 0; c < CN; ++c) dmask[c] = (d0 + c < k) ? 1.f : 0.f;
-
-  for (int64_t base = pb; base < pe; base += 64) {
-    const int nrem = (int)((pe - base) < 64 ? (pe - base) : 64);
-    int ci = 0;
-    float rv = 0.f;
-    if (lane < nrem) {
+  const bool dim_ok = d0 < k;  // dims in [k, ld) are zero by contract (see als_hip.h)
+  if (pe <= pb) return;
+  auto load_idx = [&](int64_t base, int& ci, float& rv) {
+    ci = 0;
+    rv = 0.f;
+    if (base + lane < pe) {
       ci = IDENT ? (int)(base + lane) : col[base + lane];
       rv = IDENT ? 1.f : val[base + lane];
     }
+  };
+  int ci_c, ci_n;
+  float rv_c, rv_n;
+  load_idx(pb, ci_c, rv_c);
+  load_idx(pb + 64, ci_n, rv_n);
+  float yA[8][CN], yB[8][CN];
+  int nrem = (int)((pe - pb) < 64 ? (pe - pb) : 64);
+  gather_half<CN>(yA, ci_c, 0, nrem, Y, ld, d0, dim_ok);
+  for (int64_t base = pb; base < pe; base += 64) {
+    const int64_t nbase = base + 64;
+    const int nrem_n = nbase < pe ? (int)((pe - nbase) < 64 ? (pe - nbase) : 64) : 0;
+    if (32 < nrem) gather_half<CN>(yB, ci_c, 32, nrem, Y, ld, d0, dim_ok);
     floatx4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
     float bf[CN];
 #pragma unroll
     for (int c = 0; c < CN; ++c) bf[c] = 0.f;
-    // Two halves of 32 ratings; each issues its 8 row gathers before its MFMAs.
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h * 32 < nrem) {  // wave-uniform
-        float y[8][CN];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int src = 32 * h + 4 * t + q;
-          const int s = __shfl(ci, src);
-          if (src < nrem && dim_ok) {
-            load_dims<CN>(Y + (int64_t)s * ld + d0, y[t]);
-          } else {
-#pragma unroll
-            for (int c = 0; c < CN; ++c) y[t][c] = 0.f;
-          }
-        }
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          if (32 * h + 16 * g < nrem) {  // wave-uniform: skip empty 16-rating groups
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int t = 4 * g + j;
-              const float r = __shfl(rv, 32 * h + 4 * t + q);
-              float ym[CN], ya[CN];
-              float wb;
-#pragma unroll
-              for (int c = 0; c < CN; ++c) ym[c] = y[t][c] * dmask[c];
-              if constexpr (IMPLICIT) {
-                const float c1 = alpha * fabsf(r);
-                wb = r > 0.f ? 1.f + c1 : 0.f;
-#pragma unroll
-                for (int c = 0; c < CN; ++c) ya[c] = c1 * ym[c];
-              } else {
-                wb = r;
-#pragma unroll
-                for (int c = 0; c < CN; ++c) ya[c] = ym[c];
-              }
-              int tt = 0;
-#pragma unroll
-              for (int c1 = 0; c1 < CN; ++c1) {
-#pragma unroll
-                for (int c2 = c1; c2 < CN; ++c2) {
-                  acc[tt] =
-                      __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c1], ym[c2], acc[tt], 0, 0, 0);
-                  ++tt;
-                }
-              }
-#pragma unroll
-              for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, ym[c], bf[c]);
-            }
-          }
-        }
-      }
-    }
+    mfma_half<CN, IMPLICIT>(yA, rv_c, 0, nrem, alpha, acc, bf);
+    if (nrem_n > 0) gather_half<CN>(yA, ci_n, 0, nrem_n, Y, ld, d0, dim_ok);
+    if (32 < nrem) mfma_half<CN, IMPLICIT>(yB, rv_c, 32, nrem, alpha, acc, bf);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) a64[t][r] += (double)acc[t][r];
+      for (int r = 0; r < 4; ++r) tot[t][r] += (AccT)acc[t][r];
     }
 #pragma unroll
-    for (int c = 0; c < CN; ++c) b64[c] += (double)bf[c];
-    if constexpr (IMPLICIT) npos += __popcll(__ballot(lane < nrem && rv > 0.f));
+    for (int c = 0; c < CN; ++c) btot[c] += (AccT)bf[c];
+    if constexpr (IMPLICIT) npos += __popcll(__ballot(lane < nrem && rv_c > 0.f));
+    ci_c = ci_n;
+    rv_c = rv_n;
+    nrem = nrem_n;
+    if (nrem_n > 0) load_idx(nbase + 64, ci_n, rv_n);
   }
 }
 
@@ -220,63 +247,12 @@ __device__ __forceinline__ float readlane_t(float v, int l) {
 }
 __device__ __forceinline__ double readlane_t(double v, int l) { return readlane_f64(v, l); }
 
-// Row-per-lane LDL^T factorisation of the packed SPD matrix P (KP x KP, type T)
-// with the rhs (b[lane]) carried as an augmented column, then D^-1 and the
-// back substitution L^T x = z.  Mathematically the solve of Spark's dppsv
-// (Cholesky); the square-root-free form takes one reciprocal per pivot off
-// the dependency chain, and the pivot column is broadcast UNSCALED so its LDS
-// round trip overlaps that reciprocal.  T = float for explicit feedback (the
-// systems have cond ~ (lambda + |y|^2)/lambda; measured fp32 error ~1e-6 vs the
-// 1e-4 parity bar), T = double for implicit feedback (alpha-weighted systems
-// can be far worse conditioned).  One wavefront per workgroup, so
-// __syncthreads() is only an LDS wait plus a scheduling fence.
-template <int KP, class T>
-__device__ __forceinline__ bool ldl_solve(T* __restrict__ P, T* __restrict__ cb, T b, int k,
-                                          float* __restrict__ xrow, int ld) {
-  const int lane = threadIdx.x & 63;
-  const int rb = lane < KP ? lane * (lane + 1) / 2 : 0;
-  T a[KP];
-#pragma unroll
-  for (int j = 0; j < KP; ++j) a[j] = P[rb + j];  // entries j > lane are never used
-  T myrd = T(0);
-  bool ok = true;
-#pragma unroll
-  for (int p = 0; p < KP; ++p) {
-    cb[lane] = a[p];                       // raw column p: A'[lane][p]
-    const T d = readlane_t(a[p], p);       // pivot D[p]
-    ok = ok && (d > T(0));
-    const T rd = rcp_t(d);
-    const T l = a[p] * rd;                 // L[lane][p] (lane p: 1)
-    a[p] = l;                              // row `lane` of L, written back after the loop
-    const T bp = readlane_t(b, p);         // z[p] * D[p] (forward elimination)
-    if (lane == p) myrd = rd;
-    if (lane > p) b -= l * bp;
-    __syncthreads();
-#pragma unroll
-    for (int j = p + 1; j < KP; ++j) a[j] -= l * cb[j];
-    __syncthreads();
-  }
-  // L (strict lower) back to P, z = D^-1 y, then L^T x = z by columns.
-#pragma unroll
-  for (int j = 0; j < KP; ++j)
-    if (j < lane && lane < KP) P[rb + j] = a[j];
-  __syncthreads();
-  b *= myrd;
-  T x = T(0);
-#pragma unroll
-  for (int kk = KP - 1; kk >= 0; --kk) {
-    const int off = kk * (kk + 1) / 2;
-    const T lk = lane < kk ? P[off + lane] : T(0);
-    const T xk = readlane_t(b, kk);
-    if (lane == kk) x = xk;
-    b -= lk * xk;
-  }
-  if (!ok) x = T(0);
-  for (int d = lane; d < ld; d += 64) xrow[d] = (d < k) ? (float)x : 0.f;
-  return ok;
-}
-
-// Panel-blocked form of ldl_solve (same arithmetic, PW = 4 columns per panel):
+// Row-per-lane LDL^T of the packed SPD matrix P (KP x KP, type T) with the rhs
+// (b[lane]) carried as an augmented column, then D^-1 and the back substitution
+// L^T x = z.  The square-root-free form of Spark's dppsv (Cholesky) solve: one
+// reciprocal per pivot on the dependency chain.  Used in fp64 for implicit
+// feedback (alpha-weighted systems can be far worse conditioned than the
+// lambda*n-regularised explicit ones).  Panel-blocked (PW = 4 columns):
 // inside a panel each pivot and each in-panel update use scalar broadcasts
 // (v_readlane) only; the trailing update of the remaining columns is one LDS
 // round trip per panel (each lane publishes its 4 unscaled panel entries as one
@@ -352,14 +328,16 @@ __device__ __forceinline__ bool ldl_blocked(T* __restrict__ P, T* __restrict__ c
 // (A[t] = tile (I, J), I <= J; dims permuted so that block I holds the dims
 // d = 16-index * CN + I).  Any symmetric permutation is a valid pivot order, so
 // the matrix is factored as A = U^T D U (U unit upper) in that block order:
-//   for K: factor B_KK = U_KK^T D_K U_KK              (16x16, row-per-lane, 16 lanes)
+//   for K: factor B_KK = U_KK^T D_K U_KK and forward-solve the rhs block
+//                                                    (16x16, row per lane, v_readlane broadcasts)
 //          W_KJ = U_KK^-T B_KJ, U_KJ = D_K^-1 W_KJ     (TRSM, one lane per column)
 //          B_IJ -= U_KI^T W_KJ   for K < I <= J        (v_mfma_f32_16x16x4_f32, 4 per tile)
-// The rhs rides along as one more TRSM column (forward substitution), then a
-// block back substitution finishes x.  The O(k^3) trailing work runs on the
-// MFMA pipe; the VALU keeps only the 16-wide diagonal factorisations and TRSMs.
-// LDS (floats): U tiles NT*256 (diagonal slots hold L_K rows) | stage/W NB*320 |
-// D, b, z, x 4*16*NB.
+//          b_J  -= U_KJ^T z_K                          (TRSM lanes)
+// then a block back substitution x_K = U_KK^-1 (D_K^-1 z_K - sum_J U_KJ x_J).
+// The O(k^3) trailing work runs on the MFMA pipe; the VALU keeps only the
+// 16-wide diagonal factorisations and TRSMs.
+// LDS (floats): U tiles NT*256 (diagonal slots: column-major L_K) |
+// stage/W NB*320 | D, b, z, x 4*16*NB.
 // ---------------------------------------------------------------------------
 template <int CN>
 struct TileLds {
@@ -373,13 +351,35 @@ __host__ __device__ constexpr int tile_index(int nb, int i, int j) {
   return i * nb - i * (i - 1) / 2 + (j - i);
 }
 
+// ata[ii] += lambda (explicit, fp32 tiles); padded dims get an identity row.
 template <int CN>
-__device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const double (&b64)[CN],
+__device__ __forceinline__ void regularise_f32(floatx4 (&A)[Cfg<CN>::NT], float lam, int k) {
+  int tt = 0;
+#pragma unroll
+  for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+    for (int c2 = c1; c2 < CN; ++c2) {
+      if (c1 == c2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int i, j;
+          tile_ij<CN>(c1, c2, r, i, j);
+          if (i == j) A[tt][r] = (i < k) ? A[tt][r] + lam : 1.f;
+        }
+      }
+      ++tt;
+    }
+  }
+}
+
+template <int CN>
+__device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const float (&bq)[CN],
                                                float* __restrict__ lds, int k,
                                                float* __restrict__ xrow, int ld) {
   typedef TileLds<CN> Lo;
   constexpr int NB = CN;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int i = lane & 15;  // row owned in the 16-wide steps (lanes >= 16 mirror)
   float* Ust = lds + Lo::U;
   float* St = lds + Lo::S;
   float* Dv = lds + Lo::D;
@@ -388,7 +388,7 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
   float* xv = lds + Lo::X;
   if (q == 0) {
 #pragma unroll
-    for (int c = 0; c < CN; ++c) bv[c * 16 + m] = (float)b64[c];
+    for (int c = 0; c < CN; ++c) bv[c * 16 + m] = bq[c];
   }
   bool ok = true;
 #pragma unroll
@@ -401,15 +401,14 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
           make_float4(v[0], v[1], v[2], v[3]);
     }
     __syncthreads();
-    // (b) LDL^T of the diagonal block, row `i` per lane (lanes >= 16 mirror lanes 0..15).
-    //     Broadcasts are v_readlane (no LDS round trip on the 16-step pivot chain).
-    const int i = lane & 15;
+    // (b) LDL^T of the diagonal block with the rhs block as augmented column.
     float a[16];
 #pragma unroll
     for (int c4 = 0; c4 < 4; ++c4) {
       const float4 v = *reinterpret_cast<const float4*>(St + i * 20 + 4 * c4);
       a[4 * c4] = v.x; a[4 * c4 + 1] = v.y; a[4 * c4 + 2] = v.z; a[4 * c4 + 3] = v.w;
     }
+    float bb = bv[K * 16 + i];
     float myd = 1.f;
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
@@ -418,84 +417,85 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
       float u[16];
 #pragma unroll
       for (int j = p + 1; j < 16; ++j) u[j] = readlane_t(a[p], j);  // A'[j][p]
+      const float bp = readlane_t(bb, p);
       const float l = a[p] * rcp_t(d);                                 // L[i][p]
 #pragma unroll
       for (int j = p + 1; j < 16; ++j) a[j] = fmaf(-l, u[j], a[j]);
+      if (i > p) bb = fmaf(-l, bp, bb);
       a[p] = l;
       if (i == p) myd = d;
     }
-    float* Lk = Ust + 256 * tile_index(NB, K, K);  // row-major L_K rows (for the back solve)
+    float* Lt = Ust + 256 * tile_index(NB, K, K);  // Lt[c*16 + r] = L_K[r][c]
     if (lane < 16) {
       Dv[K * 16 + i] = myd;
+      zv[K * 16 + i] = bb;
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4)
-        *reinterpret_cast<float4*>(Lk + i * 16 + 4 * c4) =
-            make_float4(a[4 * c4], a[4 * c4 + 1], a[4 * c4 + 2], a[4 * c4 + 3]);
-    }
-    // (c) TRSM: lane t < 16*(NB-1-K) owns column (t&15) of block J = K+1+(t>>4);
-    //     lane 16*(NB-1-K) owns the rhs block b_K.  L[p][c] comes from lane p by readlane.
-    const int ncol = 16 * (NB - 1 - K);
-    const int Jl = K + 1 + (lane >> 4);
-    const bool is_col = lane < ncol, is_rhs = lane == ncol;
-    float w[16];
-    {
-      const float* src = is_col ? St + (Jl - K) * 320 + (lane & 15) * 20 : bv + K * 16;
-#pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
-        w[4 * c4] = v.x; w[4 * c4 + 1] = v.y; w[4 * c4 + 2] = v.z; w[4 * c4 + 3] = v.w;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-#pragma unroll
-      for (int p = c + 1; p < 16; ++p) w[p] = fmaf(-readlane_t(a[c], p), w[c], w[p]);
-    }
-    __syncthreads();  // all stage reads done before W overwrites the stage
-    if (is_col) {
-      float* Wd = St + (Jl - K - 1) * 256 + (lane & 15);
-      float* Ud = Ust + 256 * tile_index(NB, K, Jl) + (lane & 15);
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        Wd[c * 16] = w[c];
-        Ud[c * 16] = w[c] * rcp_t(readlane_t(myd, c));
-      }
-    } else if (is_rhs) {
-#pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4)
-        *reinterpret_cast<float4*>(zv + K * 16 + 4 * c4) =
-            make_float4(w[4 * c4], w[4 * c4 + 1], w[4 * c4 + 2], w[4 * c4 + 3]);
+      for (int c = 0; c < 16; ++c) Lt[c * 16 + i] = (c < i) ? a[c] : 0.f;
     }
     __syncthreads();
-    // (d) trailing update on the matrix cores + rhs update b_J -= U_KJ^T z_K
+    if (K + 1 < NB) {
+      // (c) TRSM: lane t < 16*(NB-1-K) owns column (t&15) of block J = K+1+(t>>4).
+      const int ncol = 16 * (NB - 1 - K);
+      const int Jl = K + 1 + (lane >> 4);
+      const bool is_col = lane < ncol;
+      float w[16];
+      {
+        const float* src = St + (is_col ? (Jl - K) : 1) * 320 + i * 20;
 #pragma unroll
-    for (int I = K + 1; I < NB; ++I) {
-      float ua[4];
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
+          w[4 * c4] = v.x; w[4 * c4 + 1] = v.y; w[4 * c4 + 2] = v.z; w[4 * c4 + 3] = v.w;
+        }
+      }
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) ua[s4] = -Ust[256 * tile_index(NB, K, I) + (4 * s4 + q) * 16 + m];
+      for (int c = 0; c < 15; ++c) {
+        float lc[16];
 #pragma unroll
-      for (int J = I; J < NB; ++J) {
-        floatx4 acc = A[tile_index(NB, I, J)];
+        for (int c4 = 0; c4 < 4; ++c4) {
+          const float4 v = *reinterpret_cast<const float4*>(Lt + c * 16 + 4 * c4);
+          lc[4 * c4] = v.x; lc[4 * c4 + 1] = v.y; lc[4 * c4 + 2] = v.z; lc[4 * c4 + 3] = v.w;
+        }
+#pragma unroll
+        for (int p = c + 1; p < 16; ++p) w[p] = fmaf(-lc[p], w[c], w[p]);
+      }
+      __syncthreads();  // all stage reads done before W overwrites the stage
+      if (is_col) {
+        float* Wd = St + (Jl - K - 1) * 256 + i;
+        float* Ud = Ust + 256 * tile_index(NB, K, Jl) + i;
+        float t = 0.f;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const float uc = w[c] * rcp_t(Dv[K * 16 + c]);
+          Wd[c * 16] = w[c];
+          Ud[c * 16] = uc;
+          t = fmaf(uc, zv[K * 16 + c], t);
+        }
+        bv[Jl * 16 + i] -= t;  // rhs trailing update b_J -= U_KJ^T z_K
+      }
+      __syncthreads();
+      // (d) trailing update on the matrix cores
+#pragma unroll
+      for (int I = K + 1; I < NB; ++I) {
+        float ua[4];
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              ua[s4], St[(J - K - 1) * 256 + (4 * s4 + q) * 16 + m], acc, 0, 0, 0);
-        A[tile_index(NB, I, J)] = acc;
-      }
-    }
-    if (is_col) {
-      const float* Uc = Ust + 256 * tile_index(NB, K, Jl) + (lane & 15);
-      float t = 0.f;
+          ua[s4] = -Ust[256 * tile_index(NB, K, I) + (4 * s4 + q) * 16 + m];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) t = fmaf(Uc[c * 16], zv[K * 16 + c], t);
-      bv[Jl * 16 + (lane & 15)] -= t;
+        for (int J = I; J < NB; ++J) {
+          floatx4 acc = A[tile_index(NB, I, J)];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                ua[s4], St[(J - K - 1) * 256 + (4 * s4 + q) * 16 + m], acc, 0, 0, 0);
+          A[tile_index(NB, I, J)] = acc;
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
   // (e) block back substitution: x_K = U_KK^-1 (D_K^-1 z_K - sum_{J>K} U_KJ x_J)
 #pragma unroll
   for (int K = NB - 1; K >= 0; --K) {
-    const int i = lane & 15;
     float v = zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
 #pragma unroll
     for (int J = K + 1; J < NB; ++J) {
@@ -503,10 +503,10 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
 #pragma unroll
       for (int j = 0; j < 16; ++j) v = fmaf(-Ur[j], xv[J * 16 + j], v);
     }
-    const float* Lk = Ust + 256 * tile_index(NB, K, K) + i;
-    float ur[16];  // ur[j] = U_KK[i][j] = L_K[j][i]
+    const float* Lr = Ust + 256 * tile_index(NB, K, K) + i * 16;  // U_KK[i][j] = L_K[j][i]
+    float ur[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ur[j] = Lk[j * 16];
+    for (int j = 0; j < 16; ++j) ur[j] = Lr[j];
     float x = 0.f;
 #pragma unroll
     for (int j = 15; j >= 0; --j) {
@@ -525,11 +525,6 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
   return ok;
 }
 
-template <bool IMPLICIT>
-struct SolvePrec { typedef float T; };
-template <>
-struct SolvePrec<true> { typedef double T; };
-
 template <int CN, bool IMPLICIT>
 struct SmemBytes {
   static constexpr int value = IMPLICIT
@@ -537,59 +532,84 @@ struct SmemBytes {
       : (int)sizeof(float) * TileLds<CN>::SIZE;
 };
 
-// Shared tail: cross-slot rhs reduce, regularise (fp64), then
-//   explicit: fp32 tiles -> block LDL^T on the matrix cores (tile_ldl_solve)
-//   implicit: fp64 packed rows -> row-per-lane LDL^T (ldl_blocked<double>)
-template <int CN, bool IMPLICIT>
-__device__ __forceinline__ void finish_and_solve(double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
-                                                 int64_t n_reg, unsigned char* smem, int k,
-                                                 float reg, const double* __restrict__ yty,
-                                                 float* __restrict__ xrow, int ld, int row,
-                                                 int32_t* __restrict__ status) {
-  constexpr int KP = Cfg<CN>::KP, NT = Cfg<CN>::NT;
+template <bool IMPLICIT>
+struct AccType { typedef float T; };
+template <>
+struct AccType<true> { typedef double T; };
+
+// Explicit tail: rhs reduce over q, regularise, block LDL^T on the matrix cores.
+template <int CN>
+__device__ __forceinline__ bool finish_explicit(float (&tot)[Cfg<CN>::NT][4], float (&bt)[CN],
+                                                int64_t n_reg, unsigned char* smem, int k,
+                                                float reg, float* __restrict__ xrow, int ld) {
+  constexpr int NT = Cfg<CN>::NT;
+#pragma unroll
+  for (int c = 0; c < CN; ++c) {
+    bt[c] += __shfl_xor(bt[c], 16);
+    bt[c] += __shfl_xor(bt[c], 32);
+  }
+  floatx4 A[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) A[t][r] = tot[t][r];
+  regularise_f32<CN>(A, (float)((double)reg * (double)n_reg), k);
+  return tile_ldl_solve<CN>(A, bt, reinterpret_cast<float*>(smem), k, xrow, ld);
+}
+
+// Implicit tail: fp64 throughout (YtY merge, regularise, row-per-lane LDL^T).
+template <int CN>
+__device__ __forceinline__ bool finish_implicit(double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
+                                                int64_t n_reg, unsigned char* smem, int k,
+                                                float reg, const double* __restrict__ yty,
+                                                float* __restrict__ xrow, int ld) {
+  constexpr int KP = Cfg<CN>::KP;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
 #pragma unroll
   for (int c = 0; c < CN; ++c) {
     b64[c] += shfl_xor_f64(b64[c], 16);
     b64[c] += shfl_xor_f64(b64[c], 32);
   }
-  regularise<CN, IMPLICIT>(a64, (double)reg * (double)n_reg, k, yty);
-  bool ok;
-  if constexpr (!IMPLICIT) {
-    floatx4 A[NT];
+  regularise<CN, true>(a64, (double)reg * (double)n_reg, k, yty);
+  double* P = reinterpret_cast<double*>(smem);
+  double* cb = P + Cfg<CN>::NP;
+  pack_gram<CN, double>(a64, P);
+  if (q == 0) {
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) A[t][r] = (float)a64[t][r];
-    ok = tile_ldl_solve<CN>(A, b64, reinterpret_cast<float*>(smem), k, xrow, ld);
-  } else {
-    double* P = reinterpret_cast<double*>(smem);
-    double* cb = P + Cfg<CN>::NP;
-    pack_gram<CN, double>(a64, P);
-    if (q == 0) {
-#pragma unroll
-      for (int c = 0; c < CN; ++c) cb[m * CN + c] = b64[c];
-    }
-    __syncthreads();
-    const double b = lane < KP ? cb[lane] : 0.0;
-    __syncthreads();
-    ok = ldl_blocked<KP, double>(P, cb, b, k, xrow, ld);
+    for (int c = 0; c < CN; ++c) cb[m * CN + c] = b64[c];
   }
-  if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
+  __syncthreads();
+  const double b = lane < KP ? cb[lane] : 0.0;
+  __syncthreads();
+  return ldl_blocked<KP, double>(P, cb, b, k, xrow, ld);
 }
 
-template <int CN>
+template <int CN, bool IMPLICIT, class AccT>
+__device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], AccT (&bt)[CN],
+                                                 int64_t n_reg, unsigned char* smem, int k,
+                                                 float reg, const double* __restrict__ yty,
+                                                 float* __restrict__ xrow, int ld, int row,
+                                                 int32_t* __restrict__ status) {
+  bool ok;
+  if constexpr (IMPLICIT)
+    ok = finish_implicit<CN>(tot, bt, n_reg, smem, k, reg, yty, xrow, ld);
+  else
+    ok = finish_explicit<CN>(tot, bt, n_reg, smem, k, reg, xrow, ld);
+  if (!ok && (threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
+}
+
+template <int CN, class AccT>
 __device__ __forceinline__ void store_slot(double* __restrict__ slot,
-                                           const double (&a64)[Cfg<CN>::NT][4],
-                                           const double (&b64)[CN], int npos) {
+                                           const AccT (&tot)[Cfg<CN>::NT][4],
+                                           const AccT (&bt)[CN], int npos) {
   constexpr int NT = Cfg<CN>::NT;
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = a64[t][r];
+    for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = (double)tot[t][r];
 #pragma unroll
-  for (int c = 0; c < CN; ++c) slot[(NT * 4 + c) * 64 + lane] = b64[c];
+  for (int c = 0; c < CN; ++c) slot[(NT * 4 + c) * 64 + lane] = (double)bt[c];
   slot[(NT * 4 + CN) * 64 + lane] = (double)npos;
 }
 
@@ -608,8 +628,20 @@ __device__ __forceinline__ void add_slot(const double* __restrict__ slot,
   npos += (int)slot[(NT * 4 + CN) * 64 + lane];
 }
 
+template <int CN, class AccT>
+__device__ __forceinline__ void zero_acc(AccT (&tot)[Cfg<CN>::NT][4], AccT (&bt)[CN]) {
+#pragma unroll
+  for (int t = 0; t < Cfg<CN>::NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tot[t][r] = AccT(0);
+#pragma unroll
+  for (int c = 0; c < CN; ++c) bt[c] = AccT(0);
+}
+
 // Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) first,
 // then whole light rows (Gram + solve fused, A never leaves the CU).
+// Explicit: per-task Gram sums in fp32 (<= 2048 ratings: 64-rating exact-product
+// MFMA blocks summed in fp32), cross-chunk sums in fp64.  Implicit: fp64.
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -619,32 +651,27 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
+  typedef typename AccType<IMPLICIT>::T AccT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
   const int task = blockIdx.x;
-  double a64[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
-  double b64[CN];
-#pragma unroll
-  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  AccT tot[NT][4], bt[CN];
+  zero_acc<CN, AccT>(tot, bt);
   int npos = 0;
   if (task < n_chunks) {
-    gram_accumulate<CN, IMPLICIT, false>(col, val, chunk_begin[task], chunk_end[task], Y, ld, k,
-                                         alpha, a64, b64, npos);
-    store_slot<CN>(slots + (int64_t)task * Cfg<CN>::SLOT, a64, b64, npos);
+    gram_accumulate<CN, IMPLICIT, false, AccT>(col, val, chunk_begin[task], chunk_end[task], Y,
+                                               ld, k, alpha, tot, bt, npos);
+    store_slot<CN, AccT>(slots + (int64_t)task * Cfg<CN>::SLOT, tot, bt, npos);
     return;
   }
   const int row = light_rows[task - n_chunks];
   const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
-  gram_accumulate<CN, IMPLICIT, false>(col, val, pb, pe, Y, ld, k, alpha, a64, b64, npos);
+  gram_accumulate<CN, IMPLICIT, false, AccT>(col, val, pb, pe, Y, ld, k, alpha, tot, bt, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, smem, k, reg, yty, X + (int64_t)row * ld, ld,
-                                 row, status);
+  finish_and_solve<CN, IMPLICIT, AccT>(tot, bt, n_reg, smem, k, reg, yty, X + (int64_t)row * ld,
+                                       ld, row, status);
 }
 
-// Launch 2: heavy rows — sum their chunk slots in a fixed order, then solve.
+// Launch 2: heavy rows — sum their chunk slots in a fixed order (fp64), then solve.
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
@@ -652,44 +679,41 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
+  typedef typename AccType<IMPLICIT>::T AccT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
-  double a64[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
-  double b64[CN];
-#pragma unroll
-  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  double a64[NT][4], b64[CN];
+  zero_acc<CN, double>(a64, b64);
   int npos = 0;
   for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
     add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
-  finish_and_solve<CN, IMPLICIT>(a64, b64, n_reg, smem, k, reg, yty, X + (int64_t)row * ld, ld,
-                                 row, status);
+  AccT tot[NT][4], bt[CN];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tot[t][r] = (AccT)a64[t][r];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) bt[c] = (AccT)b64[c];
+  finish_and_solve<CN, IMPLICIT, AccT>(tot, bt, n_reg, smem, k, reg, yty, X + (int64_t)row * ld,
+                                       ld, row, status);
 }
 
-// K2b: YtY partial Grams over row chunks of Y (unweighted, identity gather).
+// K2b: YtY partial Grams over row chunks of Y (unweighted, identity gather), fp64.
 template <int CN>
 __global__ __launch_bounds__(64, 2) void yty_partial_kernel(const float* __restrict__ Y, int64_t n,
                                                             int ld, int k,
                                                             double* __restrict__ slots) {
   constexpr int NT = Cfg<CN>::NT;
-  double a64[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
-  double b64[CN];
-#pragma unroll
-  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  double a64[NT][4], b64[CN];
+  zero_acc<CN, double>(a64, b64);
   int npos = 0;
   const int64_t pb = (int64_t)blockIdx.x * kYtyChunk;
   const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
-  gram_accumulate<CN, false, true>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64, b64, npos);
-  store_slot<CN>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, npos);
+  gram_accumulate<CN, false, true, double>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64, b64,
+                                           npos);
+  store_slot<CN, double>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, npos);
 }
 
 template <int CN>
@@ -697,14 +721,8 @@ __global__ __launch_bounds__(64) void yty_reduce_kernel(const double* __restrict
                                                         int nslots, double* __restrict__ out) {
   constexpr int NT = Cfg<CN>::NT, NP = Cfg<CN>::NP;
   __shared__ double P[NP];
-  double a64[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) a64[t][r] = 0.0;
-  double b64[CN];
-#pragma unroll
-  for (int c = 0; c < CN; ++c) b64[c] = 0.0;
+  double a64[NT][4], b64[CN];
+  zero_acc<CN, double>(a64, b64);
   int npos = 0;
   for (int s = 0; s < nslots; ++s) add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
   pack_gram<CN, double>(a64, P);

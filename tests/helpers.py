@@ -36,3 +36,13 @@ def rel_row_err(x, ref):
     num = np.linalg.norm(x - ref, axis=1)
     den = np.maximum(np.linalg.norm(ref, axis=1), 1e-6)
     return float((num / den).max())
+
+
+def report(name, value):
+    """Append a measured error to $ALS_TEST_REPORT (JSON lines) when set."""
+    import json
+    import os
+    path = os.environ.get("ALS_TEST_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": name, "value": float(value)}) + "\n")

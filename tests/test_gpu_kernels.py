@@ -19,7 +19,7 @@ import torch
 
 import als_mi355x.engine as E
 from oracle import als_oracle as O
-from helpers import planted, rel_row_err
+from helpers import planted, rel_row_err, report
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -96,14 +96,18 @@ def test_half_sweep_parity(rank, implicit):
                          U0, reg, implicit, alpha)
     V = core.V.cpu().numpy()
     assert np.all(V[:, rank:] == 0.0)
-    assert rel_row_err(V[:, :rank], V_ref) <= 1e-4
+    ev = rel_row_err(V[:, :rank], V_ref)
+    report(f"half_sweep_items[rank={rank},implicit={implicit}]", ev)
+    assert ev <= 1e-4
     # and the user side from the oracle's V (identical source factors)
     core.V[:, :rank] = torch.as_tensor(V_ref).to(DEV)
     core.half_sweep_users(reg, implicit, alpha)
     ub = core.user_block
     U_ref = O.half_sweep(ub.row_ptr.cpu().numpy(), ub.col.cpu().numpy(), ub.val.cpu().numpy(),
                          V_ref, reg, implicit, alpha)
-    assert rel_row_err(core.U[:, :rank].cpu().numpy(), U_ref) <= 1e-4
+    eu = rel_row_err(core.U[:, :rank].cpu().numpy(), U_ref)
+    report(f"half_sweep_users[rank={rank},implicit={implicit}]", eu)
+    assert eu <= 1e-4
 
 
 @pytest.mark.parametrize("rank", [3, 16, 40, 64])

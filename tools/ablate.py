@@ -40,12 +40,11 @@ def main():
     torch.cuda.synchronize()
     st = torch.zeros(1, dtype=torch.int32, device=dev)
     names = {0: "full (tile LDL)", 1: "gram only", 2: "solve only (tile LDL)",
-             3: "solve only (unblocked)", 4: "full (unblocked LDL)",
              5: "half gram / half solve"}
     for side, blk, Y, X in (("item", core.item_block, core.U, core.V),
                             ("user", core.user_block, core.V, core.U)):
         X2 = torch.empty_like(X)
-        for mode in (0, 1, 2, 3, 4, 5):
+        for mode in (0, 1, 2, 5):
             times = []
             for rep in range(4):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -212,6 +212,9 @@ def _train_triples(core):
 
 def run_distributed(args):
     from als_mi355x.distributed import ShardedALS
+    for k_, v_ in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"),
+                   ("WORLD_SIZE", "1"), ("LOCAL_RANK", "0")):
+        os.environ.setdefault(k_, v_)
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
@@ -272,8 +275,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rmse", dest="rmse", action="store_false")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the sharded (RCCL) code path even with one rank")
     args = ap.parse_args()
-    if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.force_dist:
         run_distributed(args)
     else:
         run_single(args)

@@ -1,0 +1,113 @@
+"""Multi-process (world_size 2, gloo, CPU) test of the sharded ALS coordination
+(als_mi355x.distributed.ShardedALS): id-space agreement, nnz-balanced row
+ranges, the one-time all_to_all rating routing, padded factor layout, per
+half-sweep all_gather and the implicit YtY all_reduce.
+
+The HIP kernels cannot run on a CPU, so the arithmetic is injected: the test
+passes `OracleKernels` (the CPU oracle behind ShardedALS's kernel interface).
+The result must equal a single-process oracle fit from the same initial
+factors — i.e. sharding changes nothing but where rows are solved."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import planted
+
+
+class OracleKernels:
+    """CPU oracle behind the kernel interface of ShardedALS (test only)."""
+
+    def __init__(self):
+        from oracle import als_oracle as O
+        self.O = O
+
+    def index_build(self, ids, id_space):
+        mp_, uniq = self.O.index_build(ids.numpy(), id_space)
+        return torch.as_tensor(mp_), torch.as_tensor(uniq), len(uniq)
+
+    def build_block(self, rows, cols, vals, n_rows, n_cols):
+        ptr, idx, val = self.O.csr_build(rows.numpy(), cols.numpy(), vals.numpy(), n_rows)
+        return (ptr, idx, val)
+
+    def yty(self, Y, n, rank):
+        return torch.as_tensor(self.O.yty(Y[:n, :rank].numpy()))
+
+    def solve_half(self, block, Y, X, rank, reg, implicit, alpha, yty, status):
+        ptr, idx, val = block
+        n = len(ptr) - 1
+        if n == 0:
+            return
+        A, b, ne = self.O.normal_equations(ptr, idx, val, Y[:, :rank].numpy(), implicit, alpha)
+        x = self.O.solve(A, b, ne, reg, None if yty is None else yty.numpy())
+        X[:n, :rank] = torch.as_tensor(x)
+
+    def ld(self, rank):
+        return rank
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, implicit, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x.distributed import ShardedALS
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
+    if implicit:
+        r = (r - 2.5).astype(np.float32)
+    # arbitrary (non-aligned) input sharding: interleaved ratings
+    sel = np.arange(len(u)) % world == rank
+    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
+    from oracle import als_oracle as O
+    n_users = len(np.unique(u))
+    U0 = O.initialize(n_users, 6, seed=2)
+    K.fit(6, 3, 0.1, implicit=implicit, alpha=2.0, U0_global=U0)
+    uid, Uf = K.user_factors()
+    iid, Vf = K.item_factors()
+    if rank == 0:
+        np.savez(os.path.join(out_dir, f"dist_{int(implicit)}.npz"), uid=uid.numpy(),
+                 U=Uf.numpy(), iid=iid.numpy(), V=Vf.numpy(), nnz=K.nnz,
+                 u_starts=K.users.starts.numpy(), i_starts=K.items.starts.numpy(),
+                 local=[K.user_rows, K.item_rows])
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("implicit", [False, True])
+def test_sharded_als_matches_single_process(tmp_path, implicit):
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), implicit, str(tmp_path)), nprocs=world,
+             join=True)
+    d = np.load(tmp_path / f"dist_{int(implicit)}.npz")
+    from oracle import als_oracle as O
+    u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
+    if implicit:
+        r = (r - 2.5).astype(np.float32)
+    assert int(d["nnz"]) == len(u)
+    U0 = O.initialize(len(np.unique(u)), 6, seed=2)
+    U, V, umap, imap, uids, iids = O.train(u, i, r, 6, 3, 0.1, implicit=implicit, alpha=2.0,
+                                           U0=U0)
+    np.testing.assert_array_equal(d["uid"], uids)
+    np.testing.assert_array_equal(d["iid"], iids)
+    np.testing.assert_allclose(d["U"], U, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(d["V"], V, rtol=1e-5, atol=1e-6)
+    # both ranks got a share of the rows; ranges cover all rows
+    assert d["u_starts"][0] == 0 and d["u_starts"][-1] == len(uids)
+    assert d["i_starts"][-1] == len(iids)
+    assert all(x > 0 for x in np.diff(d["u_starts"]))

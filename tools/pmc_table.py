@@ -17,7 +17,7 @@ for p in ("p1", "p2"):
 seq = {p: [rows[k] for k in sorted(k for k in rows if k[0] == p)] for p in ("p1", "p2")}
 print(f"{'side':5s} {'mode':>4s} {'VALU/w':>8s} {'LDS/w':>7s} {'SALU/w':>7s} {'MFMA/w':>7s} {'lifeK':>7s} "
       f"{'act%':>5s} {'wait%':>6s} {'wInst%':>6s} {'occ':>5s} {'mfma%':>6s} {'GHz':>5s}")
-for a, b in zip(seq["p1"][3::4], seq["p2"][3::4]):
+for a, b in zip(seq["p1"][3::4], seq["p2"][3::4]):  # last of 4 reps
     w = a["SQ_WAVES"]
     side = "item" if a["grid"] < 5e6 else "user"
     life = a["SQ_WAVE_CYCLES"] / w * 4

@@ -27,6 +27,8 @@
 //    as an augmented column, followed by a column-sweep back substitution.
 #include "als_common.h"
 
+#include <utility>
+
 namespace als {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -41,11 +43,45 @@ struct Cfg {
   static constexpr int SLOT = (NT * 4 + CN + 1) * 64; // doubles per partial slot
 };
 
-static inline int cn_for_k(int k) { return k <= 16 ? 1 : (k <= 32 ? 2 : 4); }
+static inline int cn_for_k(int k) { return k <= 16 ? 1 : (k <= 32 ? 2 : (k <= 64 ? 4 : 8)); }
+
+// Compile-time loop over 0..N-1 (indices are constant expressions in the body,
+// so register arrays indexed through constexpr tables stay in registers).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// Which 16x16 Gram tiles (c1 <= c2) a wavefront accumulates.
+// FullTiles<CN>: all CN(CN+1)/2 upper tiles (one wave per task, k <= 64).
+template <int CN>
+struct FullTiles {
+  static constexpr int N = CN * (CN + 1) / 2;
+  static constexpr bool RHS = true;
+  __host__ __device__ static constexpr int c1(int t) {
+    int a = 0;
+    while (t >= CN - a) { t -= CN - a; ++a; }
+    return a;
+  }
+  __host__ __device__ static constexpr int c2(int t) {
+    int a = 0;
+    while (t >= CN - a) { t -= CN - a; ++a; }
+    return a + t;
+  }
+};
 
 template <int CN>
 __device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y)[CN]) {
-  if constexpr (CN == 4) {
+  if constexpr (CN == 8) {
+    const float4 v0 = *reinterpret_cast<const float4*>(p);
+    const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+    y[0] = v0.x; y[1] = v0.y; y[2] = v0.z; y[3] = v0.w;
+    y[4] = v1.x; y[5] = v1.y; y[6] = v1.z; y[7] = v1.w;
+  } else if constexpr (CN == 4) {
     const float4 v = *reinterpret_cast<const float4*>(p);
     y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
   } else if constexpr (CN == 2) {
@@ -76,11 +112,11 @@ __device__ __forceinline__ void gather_half(float (&y)[8][CN], int ci, int base,
   }
 }
 
-// MFMA over one gathered half-block: acc[tile] += (w_a y)(y)^T, bf += w_b y.
-template <int CN, bool IMPLICIT>
+// MFMA over one gathered half-block: acc[tile] += (w_a y)(y)^T over the tiles of
+// TS, and (if TS::RHS) bf += w_b y.
+template <int CN, class TS, bool IMPLICIT>
 __device__ __forceinline__ void mfma_half(const float (&y)[8][CN], float rv, int base, int nrem,
-                                          float alpha, floatx4 (&acc)[Cfg<CN>::NT],
-                                          float (&bf)[CN]) {
+                                          float alpha, floatx4 (&acc)[TS::N], float (&bf)[CN]) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -89,31 +125,27 @@ __device__ __forceinline__ void mfma_half(const float (&y)[8][CN], float rv, int
       for (int j = 0; j < 4; ++j) {
         const int t = 4 * g + j;
         const float r = __shfl(rv, base + 4 * t + q);
-        float ym[CN], ya[CN];
+        float ya[CN];
         float wb;
-#pragma unroll
-        for (int c = 0; c < CN; ++c) ym[c] = y[t][c];
         if constexpr (IMPLICIT) {
           const float c1 = alpha * fabsf(r);
           wb = r > 0.f ? 1.f + c1 : 0.f;
 #pragma unroll
-          for (int c = 0; c < CN; ++c) ya[c] = c1 * ym[c];
+          for (int c = 0; c < CN; ++c) ya[c] = c1 * y[t][c];
         } else {
           wb = r;
 #pragma unroll
-          for (int c = 0; c < CN; ++c) ya[c] = ym[c];
+          for (int c = 0; c < CN; ++c) ya[c] = y[t][c];
         }
-        int tt = 0;
+        static_for<TS::N>([&](auto ti) {
+          constexpr int tt = decltype(ti)::value;
+          constexpr int a = TS::c1(tt), b = TS::c2(tt);
+          acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[a], y[t][b], acc[tt], 0, 0, 0);
+        });
+        if constexpr (TS::RHS) {
 #pragma unroll
-        for (int c1 = 0; c1 < CN; ++c1) {
-#pragma unroll
-          for (int c2 = c1; c2 < CN; ++c2) {
-            acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[c1], ym[c2], acc[tt], 0, 0, 0);
-            ++tt;
-          }
+          for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, y[t][c], bf[c]);
         }
-#pragma unroll
-        for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, ym[c], bf[c]);
       }
     }
   }
@@ -126,14 +158,13 @@ __device__ __forceinline__ void mfma_half(const float (&y)[8][CN], float rv, int
 // lane's rating slot q (summed over q by the caller); npos: #ratings > 0.
 // Software pipeline: the row gathers of half-block h+1 are in flight while the
 // MFMAs of half-block h run; rating indices are loaded one 64-block ahead.
-template <int CN, bool IMPLICIT, bool IDENT, class AccT>
+template <int CN, bool IMPLICIT, bool IDENT, class AccT, class TS = FullTiles<CN>>
 __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
                                                 const float* __restrict__ val, int64_t pb,
                                                 int64_t pe, const float* __restrict__ Y, int ld,
-                                                int k, float alpha,
-                                                AccT (&tot)[Cfg<CN>::NT][4], AccT (&btot)[CN],
-                                                int& npos) {
-  constexpr int NT = Cfg<CN>::NT;
+                                                int k, float alpha, AccT (&tot)[TS::N][4],
+                                                AccT (&btot)[CN], int& npos) {
+  constexpr int NT = TS::N;
   const int lane = threadIdx.x & 63, m = lane & 15;
   const int d0 = m * CN;
   const bool dim_ok = d0 < k;  // dims in [k, ld) are zero by contract (see als_hip.h)
@@ -163,16 +194,18 @@ __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
     float bf[CN];
 #pragma unroll
     for (int c = 0; c < CN; ++c) bf[c] = 0.f;
-    mfma_half<CN, IMPLICIT>(yA, rv_c, 0, nrem, alpha, acc, bf);
+    mfma_half<CN, TS, IMPLICIT>(yA, rv_c, 0, nrem, alpha, acc, bf);
     if (nrem_n > 0) gather_half<CN>(yA, ci_n, 0, nrem_n, Y, ld, d0, dim_ok);
-    if (32 < nrem) mfma_half<CN, IMPLICIT>(yB, rv_c, 32, nrem, alpha, acc, bf);
+    if (32 < nrem) mfma_half<CN, TS, IMPLICIT>(yB, rv_c, 32, nrem, alpha, acc, bf);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) tot[t][r] += (AccT)acc[t][r];
     }
+    if constexpr (TS::RHS) {
 #pragma unroll
-    for (int c = 0; c < CN; ++c) btot[c] += (AccT)bf[c];
+      for (int c = 0; c < CN; ++c) btot[c] += (AccT)bf[c];
+    }
     if constexpr (IMPLICIT) npos += __popcll(__ballot(lane < nrem && rv_c > 0.f));
     ci_c = ci_n;
     rv_c = rv_n;
@@ -188,32 +221,6 @@ __device__ __forceinline__ void tile_ij(int c1, int c2, int r, int& i, int& j) {
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   i = (4 * q + r) * CN + c1;
   j = m * CN + c2;
-}
-
-// Complete the normal equations in fp64 registers (Spark CholeskySolver.solve:
-// ata[ii] += lambda * numExplicits; implicit: ls.merge(YtY)); padded dims get
-// an identity row so their solution is 0.
-template <int CN, bool IMPLICIT>
-__device__ __forceinline__ void regularise(double (&a64)[Cfg<CN>::NT][4], double lam, int k,
-                                           const double* __restrict__ yty) {
-  int tt = 0;
-#pragma unroll
-  for (int c1 = 0; c1 < CN; ++c1) {
-#pragma unroll
-    for (int c2 = c1; c2 < CN; ++c2) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int i, j;
-        tile_ij<CN>(c1, c2, r, i, j);
-        if constexpr (IMPLICIT) {
-          const int hi = i > j ? i : j, lo = i > j ? j : i;
-          a64[tt][r] += yty[hi * (hi + 1) / 2 + lo];
-        }
-        if (c1 == c2 && i == j) a64[tt][r] = (i < k) ? a64[tt][r] + lam : 1.0;
-      }
-      ++tt;
-    }
-  }
 }
 
 // Scatter the MFMA-layout matrix into the packed lower triangle P (type T) in LDS.
@@ -247,82 +254,8 @@ __device__ __forceinline__ float readlane_t(float v, int l) {
 }
 __device__ __forceinline__ double readlane_t(double v, int l) { return readlane_f64(v, l); }
 
-// Row-per-lane LDL^T of the packed SPD matrix P (KP x KP, type T) with the rhs
-// (b[lane]) carried as an augmented column, then D^-1 and the back substitution
-// L^T x = z.  The square-root-free form of Spark's dppsv (Cholesky) solve: one
-// reciprocal per pivot on the dependency chain.  Used in fp64 for implicit
-// feedback (alpha-weighted systems can be far worse conditioned than the
-// lambda*n-regularised explicit ones).  Panel-blocked (PW = 4 columns):
-// inside a panel each pivot and each in-panel update use scalar broadcasts
-// (v_readlane) only; the trailing update of the remaining columns is one LDS
-// round trip per panel (each lane publishes its 4 unscaled panel entries as one
-// 16-byte record, every lane streams the records of rows j > panel with
-// broadcast ds_read_b128 and applies 4 FMAs per record).  16 LDS round trips
-// instead of 64 on the pivot chain.
-template <int KP, class T>
-__device__ __forceinline__ bool ldl_blocked(T* __restrict__ P, T* __restrict__ cb, T b, int k,
-                                            float* __restrict__ xrow, int ld) {
-  constexpr int PW = 4;
-  static_assert(KP % PW == 0, "KP must be a multiple of the panel width");
-  const int lane = threadIdx.x & 63;
-  const int rb = lane < KP ? lane * (lane + 1) / 2 : 0;
-  T a[KP];
-#pragma unroll
-  for (int j = 0; j < KP; ++j) a[j] = P[rb + j];  // entries j > lane are never used
-  T myrd = T(0);
-  bool ok = true;
-#pragma unroll
-  for (int pb = 0; pb < KP; pb += PW) {
-    T l[PW], u[PW];
-#pragma unroll
-    for (int c = 0; c < PW; ++c) {
-      const int p = pb + c;
-      u[c] = a[p];                         // A'[lane][p] before elimination of p
-      const T d = readlane_t(a[p], p);     // pivot D[p]
-      ok = ok && (d > T(0));
-      const T rd = rcp_t(d);
-      l[c] = u[c] * rd;                    // L[lane][p]
-      a[p] = l[c];
-      if (lane == p) myrd = rd;
-      const T bp = readlane_t(b, p);
-      if (lane > p) b -= l[c] * bp;
-#pragma unroll
-      for (int c2 = c + 1; c2 < PW; ++c2) a[pb + c2] -= l[c] * readlane_t(u[c], pb + c2);
-    }
-    if (pb + PW < KP) {
-#pragma unroll
-      for (int c = 0; c < PW; ++c) cb[PW * lane + c] = u[c];
-      __syncthreads();  // 1-wave workgroup: an LDS wait + scheduling fence only
-#pragma unroll
-      for (int j = pb + PW; j < KP; ++j) {
-#pragma unroll
-        for (int c = 0; c < PW; ++c) a[j] -= l[c] * cb[PW * j + c];
-      }
-      __syncthreads();
-    }
-  }
-  // L (strict lower) to P, z = D^-1 y, then L^T x = z by columns.
-#pragma unroll
-  for (int j = 0; j < KP; ++j)
-    if (j < lane && lane < KP) P[rb + j] = a[j];
-  __syncthreads();
-  b *= myrd;
-  T x = T(0);
-#pragma unroll
-  for (int kk = KP - 1; kk >= 0; --kk) {
-    const int off = kk * (kk + 1) / 2;
-    const T lk = lane < kk ? P[off + lane] : T(0);
-    const T xk = readlane_t(b, kk);
-    if (lane == kk) x = xk;
-    b -= lk * xk;
-  }
-  if (!ok) x = T(0);
-  for (int d = lane; d < ld; d += 64) xrow[d] = (d < k) ? (float)x : 0.f;
-  return ok;
-}
-
 // ---------------------------------------------------------------------------
-// Block LDL^T on the matrix cores (explicit path).
+// Block LDL^T on the matrix cores.
 //
 // The regularised Gram arrives as fp32 16x16 tiles in the MFMA C layout
 // (A[t] = tile (I, J), I <= J; dims permuted so that block I holds the dims
@@ -525,76 +458,57 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
   return ok;
 }
 
-template <int CN, bool IMPLICIT>
+template <int CN>
 struct SmemBytes {
-  static constexpr int value = IMPLICIT
-      ? (int)sizeof(double) * (Cfg<CN>::NP + 64 * 4)
-      : (int)sizeof(float) * TileLds<CN>::SIZE;
+  static constexpr int value = (int)sizeof(float) * TileLds<CN>::SIZE;
 };
 
-template <bool IMPLICIT>
-struct AccType { typedef float T; };
-template <>
-struct AccType<true> { typedef double T; };
+__device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
+__device__ __forceinline__ double shfl_xor_t(double v, int m) { return shfl_xor_f64(v, m); }
 
-// Explicit tail: rhs reduce over q, regularise, block LDL^T on the matrix cores.
-template <int CN>
-__device__ __forceinline__ bool finish_explicit(float (&tot)[Cfg<CN>::NT][4], float (&bt)[CN],
-                                                int64_t n_reg, unsigned char* smem, int k,
-                                                float reg, float* __restrict__ xrow, int ld) {
-  constexpr int NT = Cfg<CN>::NT;
-#pragma unroll
-  for (int c = 0; c < CN; ++c) {
-    bt[c] += __shfl_xor(bt[c], 16);
-    bt[c] += __shfl_xor(bt[c], 32);
-  }
-  floatx4 A[NT];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) A[t][r] = tot[t][r];
-  regularise_f32<CN>(A, (float)((double)reg * (double)n_reg), k);
-  return tile_ldl_solve<CN>(A, bt, reinterpret_cast<float*>(smem), k, xrow, ld);
-}
-
-// Implicit tail: fp64 throughout (YtY merge, regularise, row-per-lane LDL^T).
-template <int CN>
-__device__ __forceinline__ bool finish_implicit(double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
-                                                int64_t n_reg, unsigned char* smem, int k,
-                                                float reg, const double* __restrict__ yty,
-                                                float* __restrict__ xrow, int ld) {
-  constexpr int KP = Cfg<CN>::KP;
-  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-#pragma unroll
-  for (int c = 0; c < CN; ++c) {
-    b64[c] += shfl_xor_f64(b64[c], 16);
-    b64[c] += shfl_xor_f64(b64[c], 32);
-  }
-  regularise<CN, true>(a64, (double)reg * (double)n_reg, k, yty);
-  double* P = reinterpret_cast<double*>(smem);
-  double* cb = P + Cfg<CN>::NP;
-  pack_gram<CN, double>(a64, P);
-  if (q == 0) {
-#pragma unroll
-    for (int c = 0; c < CN; ++c) cb[m * CN + c] = b64[c];
-  }
-  __syncthreads();
-  const double b = lane < KP ? cb[lane] : 0.0;
-  __syncthreads();
-  return ldl_blocked<KP, double>(P, cb, b, k, xrow, ld);
-}
-
+// Shared tail of a row: rhs reduce over the 4 rating slots, complete the normal
+// equations (Spark CholeskySolver.solve: ata[ii] += lambda * numExplicits;
+// implicit: ls.merge(YtY), added in fp64 before the single rounding to fp32),
+// then the block LDL^T on the matrix cores.  fp32 factorisation: the systems are
+// regularised (cond ~ (lambda + |y|^2)/lambda, measured <= 240 for implicit
+// alpha = 40 at k = 128), fp32 error ~2e-6 vs the 1e-4 parity bar.
 template <int CN, bool IMPLICIT, class AccT>
 __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], AccT (&bt)[CN],
                                                  int64_t n_reg, unsigned char* smem, int k,
                                                  float reg, const double* __restrict__ yty,
                                                  float* __restrict__ xrow, int ld, int row,
                                                  int32_t* __restrict__ status) {
-  bool ok;
-  if constexpr (IMPLICIT)
-    ok = finish_implicit<CN>(tot, bt, n_reg, smem, k, reg, yty, xrow, ld);
-  else
-    ok = finish_explicit<CN>(tot, bt, n_reg, smem, k, reg, xrow, ld);
+  constexpr int NT = Cfg<CN>::NT;
+  float bq[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) {
+    AccT v = bt[c];
+    v += shfl_xor_t(v, 16);
+    v += shfl_xor_t(v, 32);
+    bq[c] = (float)v;
+  }
+  floatx4 A[NT];
+  int tt = 0;
+#pragma unroll
+  for (int c1 = 0; c1 < CN; ++c1) {
+#pragma unroll
+    for (int c2 = c1; c2 < CN; ++c2) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if constexpr (IMPLICIT) {
+          int i, j;
+          tile_ij<CN>(c1, c2, r, i, j);
+          const int hi = i > j ? i : j, lo = i > j ? j : i;
+          A[tt][r] = (float)((double)tot[tt][r] + yty[hi * (hi + 1) / 2 + lo]);
+        } else {
+          A[tt][r] = (float)tot[tt][r];
+        }
+      }
+      ++tt;
+    }
+  }
+  regularise_f32<CN>(A, (float)((double)reg * (double)n_reg), k);
+  const bool ok = tile_ldl_solve<CN>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
   if (!ok && (threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -640,8 +554,8 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[Cfg<CN>::NT][4], AccT (&bt)
 
 // Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) first,
 // then whole light rows (Gram + solve fused, A never leaves the CU).
-// Explicit: per-task Gram sums in fp32 (<= 2048 ratings: 64-rating exact-product
-// MFMA blocks summed in fp32), cross-chunk sums in fp64.  Implicit: fp64.
+// Per-task Gram sums in fp32 (<= 2048 ratings: 64-rating exact-product MFMA
+// blocks summed in fp32), cross-chunk sums of heavy rows in fp64.
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -651,8 +565,8 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
-  typedef typename AccType<IMPLICIT>::T AccT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
+  typedef float AccT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int task = blockIdx.x;
   AccT tot[NT][4], bt[CN];
   zero_acc<CN, AccT>(tot, bt);
@@ -679,8 +593,7 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
-  typedef typename AccType<IMPLICIT>::T AccT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
   double a64[NT][4], b64[CN];
@@ -689,15 +602,8 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
     add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
-  AccT tot[NT][4], bt[CN];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tot[t][r] = (AccT)a64[t][r];
-#pragma unroll
-  for (int c = 0; c < CN; ++c) bt[c] = (AccT)b64[c];
-  finish_and_solve<CN, IMPLICIT, AccT>(tot, bt, n_reg, smem, k, reg, yty, X + (int64_t)row * ld,
-                                       ld, row, status);
+  finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
+                                         X + (int64_t)row * ld, ld, row, status);
 }
 
 // K2b: YtY partial Grams over row chunks of Y (unweighted, identity gather), fp64.

@@ -22,7 +22,7 @@ __global__ __launch_bounds__(64, 2) void ablate_kernel(const int64_t* __restrict
                                                        float* __restrict__ X, int ld, float reg,
                                                        int32_t* __restrict__ status) {
   constexpr int CN = 4, NT = Cfg<CN>::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, false>::value];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int row = rows[blockIdx.x];
   const int lane = threadIdx.x;
   float tot[NT][4], bt[CN];

@@ -42,7 +42,14 @@ from als_mi355x import engine as E  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, spec
 PEAK_HBM_GBS = 8000.0
-DOMINANT = "gram_solve_kernel<4,false>"
+
+
+def dominant_kernel(k: int, implicit: bool) -> str:
+    imp = "true" if implicit else "false"
+    if k > 64:
+        return f"gram_solve_wg_kernel<{imp}>"
+    cn = 1 if k <= 16 else (2 if k <= 32 else 4)
+    return f"gram_solve_kernel<{cn},{imp}>"
 
 
 def gram_flops(nnz: int, n_solved: int, k: int) -> float:
@@ -62,7 +69,8 @@ def load_pmc(kernel_prefix: str):
         return None
 
 
-def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.0):
+def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.0,
+                 implicit: bool = False, alpha: float = 1.0):
     """Time the C port (oracle/als_oracle.c, OpenMP) on a bounded prefix of rows of each side;
     extrapolate to ratings/s of a full iteration."""
     import numpy as np
@@ -85,7 +93,8 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
             sub_ptr = ptr[:nrow + 1].copy()
             nz = int(sub_ptr[-1])
             t0 = time.perf_counter()
-            c_oracle.half_sweep(sub_ptr, col[:nz], val[:nz], Y, reg, threads=threads)
+            c_oracle.half_sweep(sub_ptr, col[:nz], val[:nz], Y, reg, implicit=implicit,
+                                alpha=alpha, threads=threads)
             dt = time.perf_counter() - t0
             rate = nz / dt
             target = int(rate * budget_s / 2)
@@ -117,20 +126,25 @@ def run_single(args):
     core.status.zero_()
     ib, ub = core.item_block, core.user_block
 
+    imp, alpha = args.implicit, args.alpha
+
     def iteration(evs=None):
-        # Spark order: items from users, then users from items (ALS.train loop)
+        # Spark order: items from users, then users from items (ALS.train loop);
+        # implicit: YtY of the source side before each half-sweep (computeYtY)
+        yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
         if evs is not None:
             evs[0].record()
-        E.solve_half(ib, core.U, core.V, k, args.reg, False, 1.0, None, core.status, core.ws, 1)
+        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
         if evs is not None:
             evs[1].record()
-        E.solve_half(ib, core.U, core.V, k, args.reg, False, 1.0, None, core.status, core.ws, 2)
+        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 2)
+        yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
         if evs is not None:
             evs[2].record()
-        E.solve_half(ub, core.V, core.U, k, args.reg, False, 1.0, None, core.status, core.ws, 1)
+        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
         if evs is not None:
             evs[3].record()
-        E.solve_half(ub, core.V, core.U, k, args.reg, False, 1.0, None, core.status, core.ws, 2)
+        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 2)
 
     for _ in range(args.warmup):
         iteration()
@@ -152,7 +166,8 @@ def run_single(args):
     f_user = gram_flops(ub.nnz, ub.n_light, k)
     achieved = (f_item + f_user) / ((item_ms + user_ms) * 1e-3) / 1e12
     avg_launch_us = 1000.0 * (item_ms + user_ms) / 2
-    traffic = load_pmc("gram_solve_kernel")
+    dominant = dominant_kernel(k, imp)
+    traffic = load_pmc(dominant)
 
     # top-10 recommendations for all users (K5), timed with events after one warm run
     core.recommend_users(10)
@@ -163,8 +178,11 @@ def run_single(args):
     t1e.record()
     torch.cuda.synchronize()
     topk_ms = t0e.elapsed_time(t1e)
+    mode = f"implicit alpha={alpha:g}" if imp else "explicit"
+    cfg_idx = 2 if (imp and k == 128) else 1
     out = {
-        "metric": "ratings/sec per ALS iteration (rank 64)",
+        "metric": "ratings/sec per ALS iteration (rank 64)" if k == 64 and not imp
+                  else f"ratings/sec per ALS iteration (rank {k}, {mode})",
         "value": value,
         "unit": "ratings/s",
         "n_gpus": 1,
@@ -174,12 +192,13 @@ def run_single(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 MFMA gram, f64 accumulate + Cholesky",
+        "dtype": "f32",
         "data": "synthetic (seeded planted low-rank model on device; ML-25M shape)",
-        "config": {"workload": f"{args.config} explicit ALS rank {k} (BASELINE configs[1])",
+        "config": {"workload": f"{args.config} {mode} ALS rank {k} (BASELINE configs[{cfg_idx}])",
                    "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz,
-                   "rank": k, "regParam": args.reg, "parallelism": "dp1"},
-        "roofline": {"bound": "mfma", "kernel": DOMINANT,
+                   "rank": k, "regParam": args.reg, "implicitPrefs": imp, "alpha": alpha,
+                   "parallelism": "dp1"},
+        "roofline": {"bound": "mfma", "kernel": dominant,
                      "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
                      "avg_launch_us": avg_launch_us,
@@ -196,7 +215,7 @@ def run_single(args):
         rmse, n = core.rmse(*_train_triples(core))
         out["train_rmse"] = rmse
     if args.cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(core, k, args.reg, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(core, k, args.reg, args.cpu_budget, imp, alpha)
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)
@@ -251,7 +270,7 @@ def run_distributed(args):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 MFMA gram, f64 accumulate + Cholesky",
+            "dtype": "f32",
             "data": "synthetic (seeded planted model; one ML-25M-shaped user shard per rank)",
             "config": {"workload": f"{args.config} x{world} users explicit ALS rank {k} "
                                    "(weak scaling of BASELINE configs[1])",
@@ -272,6 +291,8 @@ def main():
     ap.add_argument("--config", default="ml25m", choices=sorted(D.CONFIGS))
     ap.add_argument("--rank", type=int, default=64)
     ap.add_argument("--reg", type=float, default=0.1)
+    ap.add_argument("--implicit", action="store_true", help="implicitPrefs=True (configs[2])")
+    ap.add_argument("--alpha", type=float, default=40.0)
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rmse", dest="rmse", action="store_false")

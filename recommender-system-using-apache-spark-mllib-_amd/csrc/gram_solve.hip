@@ -34,6 +34,7 @@ namespace als {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kYtyChunk = 8192;      // src rows per YtY task
+constexpr int kMaxRank = 128;
 
 template <int CN>
 struct Cfg {
@@ -56,32 +57,9 @@ __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-// Which 16x16 Gram tiles (c1 <= c2) a wavefront accumulates.
-// FullTiles<CN>: all CN(CN+1)/2 upper tiles (one wave per task, k <= 64).
-template <int CN>
-struct FullTiles {
-  static constexpr int N = CN * (CN + 1) / 2;
-  static constexpr bool RHS = true;
-  __host__ __device__ static constexpr int c1(int t) {
-    int a = 0;
-    while (t >= CN - a) { t -= CN - a; ++a; }
-    return a;
-  }
-  __host__ __device__ static constexpr int c2(int t) {
-    int a = 0;
-    while (t >= CN - a) { t -= CN - a; ++a; }
-    return a + t;
-  }
-};
-
 template <int CN>
 __device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y)[CN]) {
-  if constexpr (CN == 8) {
-    const float4 v0 = *reinterpret_cast<const float4*>(p);
-    const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
-    y[0] = v0.x; y[1] = v0.y; y[2] = v0.z; y[3] = v0.w;
-    y[4] = v1.x; y[5] = v1.y; y[6] = v1.z; y[7] = v1.w;
-  } else if constexpr (CN == 4) {
+  if constexpr (CN == 4) {
     const float4 v = *reinterpret_cast<const float4*>(p);
     y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
   } else if constexpr (CN == 2) {
@@ -92,31 +70,109 @@ __device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y
   }
 }
 
-// Gather the factor rows of one half-block (32 ratings = 8 MFMA steps) into
-// registers: step t, lane (q, m) gets dims m*CN .. m*CN+CN-1 of rating 4t+q.
+// Tile-set policy: which 16x16 Gram tiles a wavefront accumulates.
+//   N tiles; tile t is block (g1(t), g2(t)), g1 <= g2, in dims-block units
+//   (block c holds dims d = 16-index * CN + c).
+//   NC dims-blocks are gathered per rating ("local columns"; gcol(lc) = block),
+//   l1(t), l2(t) are tile t's local columns; NR rhs blocks = local columns 0..NR-1
+//   (NRA = max(NR, 1), the register array size).
+//   load(p, y, d0, k): this lane's NC values of one factor row (p = row + d0),
+//   zero for dims >= k (never reads past the row: ld % 4 == 0, k <= ld).
+// FullTiles<CN>: all CN(CN+1)/2 upper tiles (one wavefront per system, k <= 64).
 template <int CN>
-__device__ __forceinline__ void gather_half(float (&y)[8][CN], int ci, int base, int nrem,
-                                            const float* __restrict__ Y, int ld, int d0,
-                                            bool dim_ok) {
+struct FullTiles {
+  static constexpr int N = CN * (CN + 1) / 2, NC = CN, NR = CN, NRA = CN;
+  __host__ __device__ static constexpr int l1(int t) {
+    int a = 0;
+    while (t >= CN - a) { t -= CN - a; ++a; }
+    return a;
+  }
+  __host__ __device__ static constexpr int l2(int t) {
+    int a = 0;
+    while (t >= CN - a) { t -= CN - a; ++a; }
+    return a + t;
+  }
+  __host__ __device__ static constexpr int gcol(int c) { return c; }
+  __host__ __device__ static constexpr int g1(int t) { return l1(t); }
+  __host__ __device__ static constexpr int g2(int t) { return l2(t); }
+  __device__ static __forceinline__ void load(const float* __restrict__ p, float (&y)[NC], int d0,
+                                              int k) {
+    if (d0 < k) {
+      load_dims<CN>(p, y);
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) y[c] = 0.f;
+    }
+  }
+};
+
+// WgTiles<R>: wavefront R of the 4-wave workgroup that owns one k <= 128 system
+// (CN = 8, blocks H0 = 0..3, H1 = 4..7).  R0: upper(H0) 10 tiles + rhs H0;
+// R1: upper(H1) 10 tiles + rhs H1; R2: {0,1} x H1, 8 tiles; R3: {2,3} x H1.
+// Each wave gathers only the dims its tiles need (16 or 24 B per lane).
+template <int R>
+struct WgTiles {
+  static_assert(R >= 0 && R < 4, "4 waves");
+  static constexpr int N = R < 2 ? 10 : 8, NC = R < 2 ? 4 : 6, NR = R < 2 ? 4 : 0,
+                       NRA = R < 2 ? 4 : 1;
+  __host__ __device__ static constexpr int gcol(int c) {
+    return R == 0 ? c : (R == 1 ? 4 + c : (c < 2 ? 2 * (R - 2) + c : c + 2));
+  }
+  __host__ __device__ static constexpr int l1(int t) { return R < 2 ? FullTiles<4>::l1(t) : t / 4; }
+  __host__ __device__ static constexpr int l2(int t) {
+    return R < 2 ? FullTiles<4>::l2(t) : 2 + t % 4;
+  }
+  __host__ __device__ static constexpr int g1(int t) { return gcol(l1(t)); }
+  __host__ __device__ static constexpr int g2(int t) { return gcol(l2(t)); }
+  __device__ static __forceinline__ void load(const float* __restrict__ p, float (&y)[NC], int d0,
+                                              int k) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) y[c] = 0.f;
+    if constexpr (R < 2) {
+      if (d0 + 4 * R < k) {
+        const float4 v = *reinterpret_cast<const float4*>(p + 4 * R);
+        y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
+      }
+    } else {
+      constexpr int o = 2 * (R - 2);
+      if (d0 + o < k) {
+        const float2 v = *reinterpret_cast<const float2*>(p + o);
+        y[0] = v.x; y[1] = v.y;
+      }
+      if (d0 + 4 < k) {
+        const float4 v = *reinterpret_cast<const float4*>(p + 4);
+        y[2] = v.x; y[3] = v.y; y[4] = v.z; y[5] = v.w;
+      }
+    }
+  }
+};
+
+// Gather the factor rows of one half-block (32 ratings = 8 MFMA steps) into
+// registers: step t, lane (q, m) gets its TS dims among m*CN .. m*CN+CN-1 of
+// rating 4t+q.
+template <int CN, class TS>
+__device__ __forceinline__ void gather_half(float (&y)[8][TS::NC], int ci, int base, int nrem,
+                                            const float* __restrict__ Y, int ld, int d0, int k) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int src = base + 4 * t + q;
     const int s = __shfl(ci, src);
-    if (src < nrem && dim_ok) {
-      load_dims<CN>(Y + (int64_t)s * ld + d0, y[t]);
+    if (src < nrem) {
+      TS::load(Y + (int64_t)s * ld + d0, y[t], d0, k);
     } else {
 #pragma unroll
-      for (int c = 0; c < CN; ++c) y[t][c] = 0.f;
+      for (int c = 0; c < TS::NC; ++c) y[t][c] = 0.f;
     }
   }
 }
 
 // MFMA over one gathered half-block: acc[tile] += (w_a y)(y)^T over the tiles of
-// TS, and (if TS::RHS) bf += w_b y.
-template <int CN, class TS, bool IMPLICIT>
-__device__ __forceinline__ void mfma_half(const float (&y)[8][CN], float rv, int base, int nrem,
-                                          float alpha, floatx4 (&acc)[TS::N], float (&bf)[CN]) {
+// TS, and bf += w_b y over its rhs blocks.
+template <class TS, bool IMPLICIT>
+__device__ __forceinline__ void mfma_half(const float (&y)[8][TS::NC], float rv, int base,
+                                          int nrem, float alpha, floatx4 (&acc)[TS::N],
+                                          float (&bf)[TS::NRA]) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
@@ -125,27 +181,25 @@ __device__ __forceinline__ void mfma_half(const float (&y)[8][CN], float rv, int
       for (int j = 0; j < 4; ++j) {
         const int t = 4 * g + j;
         const float r = __shfl(rv, base + 4 * t + q);
-        float ya[CN];
+        float ya[TS::NC];
         float wb;
         if constexpr (IMPLICIT) {
           const float c1 = alpha * fabsf(r);
           wb = r > 0.f ? 1.f + c1 : 0.f;
 #pragma unroll
-          for (int c = 0; c < CN; ++c) ya[c] = c1 * y[t][c];
+          for (int c = 0; c < TS::NC; ++c) ya[c] = c1 * y[t][c];
         } else {
           wb = r;
 #pragma unroll
-          for (int c = 0; c < CN; ++c) ya[c] = y[t][c];
+          for (int c = 0; c < TS::NC; ++c) ya[c] = y[t][c];
         }
         static_for<TS::N>([&](auto ti) {
           constexpr int tt = decltype(ti)::value;
-          constexpr int a = TS::c1(tt), b = TS::c2(tt);
+          constexpr int a = TS::l1(tt), b = TS::l2(tt);
           acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya[a], y[t][b], acc[tt], 0, 0, 0);
         });
-        if constexpr (TS::RHS) {
 #pragma unroll
-          for (int c = 0; c < CN; ++c) bf[c] = fmaf(wb, y[t][c], bf[c]);
-        }
+        for (int c = 0; c < TS::NR; ++c) bf[c] = fmaf(wb, y[t][c], bf[c]);
       }
     }
   }
@@ -163,11 +217,10 @@ __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
                                                 const float* __restrict__ val, int64_t pb,
                                                 int64_t pe, const float* __restrict__ Y, int ld,
                                                 int k, float alpha, AccT (&tot)[TS::N][4],
-                                                AccT (&btot)[CN], int& npos) {
+                                                AccT (&btot)[TS::NRA], int& npos) {
   constexpr int NT = TS::N;
   const int lane = threadIdx.x & 63, m = lane & 15;
-  const int d0 = m * CN;
-  const bool dim_ok = d0 < k;  // dims in [k, ld) are zero by contract (see als_hip.h)
+  const int d0 = m * CN;  // dims in [k, ld) are zero by contract (see als_hip.h)
   if (pe <= pb) return;
   auto load_idx = [&](int64_t base, int& ci, float& rv) {
     ci = 0;
@@ -181,31 +234,29 @@ __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
   float rv_c, rv_n;
   load_idx(pb, ci_c, rv_c);
   load_idx(pb + 64, ci_n, rv_n);
-  float yA[8][CN], yB[8][CN];
+  float yA[8][TS::NC], yB[8][TS::NC];
   int nrem = (int)((pe - pb) < 64 ? (pe - pb) : 64);
-  gather_half<CN>(yA, ci_c, 0, nrem, Y, ld, d0, dim_ok);
+  gather_half<CN, TS>(yA, ci_c, 0, nrem, Y, ld, d0, k);
   for (int64_t base = pb; base < pe; base += 64) {
     const int64_t nbase = base + 64;
     const int nrem_n = nbase < pe ? (int)((pe - nbase) < 64 ? (pe - nbase) : 64) : 0;
-    if (32 < nrem) gather_half<CN>(yB, ci_c, 32, nrem, Y, ld, d0, dim_ok);
+    if (32 < nrem) gather_half<CN, TS>(yB, ci_c, 32, nrem, Y, ld, d0, k);
     floatx4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float bf[CN];
+    float bf[TS::NRA];
 #pragma unroll
-    for (int c = 0; c < CN; ++c) bf[c] = 0.f;
-    mfma_half<CN, TS, IMPLICIT>(yA, rv_c, 0, nrem, alpha, acc, bf);
-    if (nrem_n > 0) gather_half<CN>(yA, ci_n, 0, nrem_n, Y, ld, d0, dim_ok);
-    if (32 < nrem) mfma_half<CN, TS, IMPLICIT>(yB, rv_c, 32, nrem, alpha, acc, bf);
+    for (int c = 0; c < TS::NRA; ++c) bf[c] = 0.f;
+    mfma_half<TS, IMPLICIT>(yA, rv_c, 0, nrem, alpha, acc, bf);
+    if (nrem_n > 0) gather_half<CN, TS>(yA, ci_n, 0, nrem_n, Y, ld, d0, k);
+    if (32 < nrem) mfma_half<TS, IMPLICIT>(yB, rv_c, 32, nrem, alpha, acc, bf);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) tot[t][r] += (AccT)acc[t][r];
     }
-    if constexpr (TS::RHS) {
 #pragma unroll
-      for (int c = 0; c < CN; ++c) btot[c] += (AccT)bf[c];
-    }
+    for (int c = 0; c < TS::NR; ++c) btot[c] += (AccT)bf[c];
     if constexpr (IMPLICIT) npos += __popcll(__ballot(lane < nrem && rv_c > 0.f));
     ci_c = ci_n;
     rv_c = rv_n;
@@ -512,44 +563,47 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
   if (!ok && (threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
 }
 
-template <int CN, class AccT>
-__device__ __forceinline__ void store_slot(double* __restrict__ slot,
-                                           const AccT (&tot)[Cfg<CN>::NT][4],
-                                           const AccT (&bt)[CN], int npos) {
-  constexpr int NT = Cfg<CN>::NT;
+// Partial-sum slot of one task: N tiles x 4 accumulator rows, NRA rhs values and
+// the positive-rating count, each as 64 lane-contiguous doubles.
+template <int N, int NRA>
+struct Slot {
+  static constexpr int SIZE = (N * 4 + NRA + 1) * 64;
+};
+
+template <int N, int NRA, class AccT>
+__device__ __forceinline__ void store_slot(double* __restrict__ slot, const AccT (&tot)[N][4],
+                                           const AccT (&bt)[NRA], int npos) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < N; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = (double)tot[t][r];
 #pragma unroll
-  for (int c = 0; c < CN; ++c) slot[(NT * 4 + c) * 64 + lane] = (double)bt[c];
-  slot[(NT * 4 + CN) * 64 + lane] = (double)npos;
+  for (int c = 0; c < NRA; ++c) slot[(N * 4 + c) * 64 + lane] = (double)bt[c];
+  slot[(N * 4 + NRA) * 64 + lane] = (double)npos;
 }
 
-template <int CN>
-__device__ __forceinline__ void add_slot(const double* __restrict__ slot,
-                                         double (&a64)[Cfg<CN>::NT][4], double (&b64)[CN],
-                                         int& npos) {
-  constexpr int NT = Cfg<CN>::NT;
+template <int N, int NRA>
+__device__ __forceinline__ void add_slot(const double* __restrict__ slot, double (&a64)[N][4],
+                                         double (&b64)[NRA], int& npos) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < N; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) a64[t][r] += slot[(t * 4 + r) * 64 + lane];
 #pragma unroll
-  for (int c = 0; c < CN; ++c) b64[c] += slot[(NT * 4 + c) * 64 + lane];
-  npos += (int)slot[(NT * 4 + CN) * 64 + lane];
+  for (int c = 0; c < NRA; ++c) b64[c] += slot[(N * 4 + c) * 64 + lane];
+  npos += (int)slot[(N * 4 + NRA) * 64 + lane];
 }
 
-template <int CN, class AccT>
-__device__ __forceinline__ void zero_acc(AccT (&tot)[Cfg<CN>::NT][4], AccT (&bt)[CN]) {
+template <int N, int NRA, class AccT>
+__device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 #pragma unroll
-  for (int t = 0; t < Cfg<CN>::NT; ++t)
+  for (int t = 0; t < N; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tot[t][r] = AccT(0);
 #pragma unroll
-  for (int c = 0; c < CN; ++c) bt[c] = AccT(0);
+  for (int c = 0; c < NRA; ++c) bt[c] = AccT(0);
 }
 
 // Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) first,
@@ -569,12 +623,12 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int task = blockIdx.x;
   AccT tot[NT][4], bt[CN];
-  zero_acc<CN, AccT>(tot, bt);
+  zero_acc<NT, CN, AccT>(tot, bt);
   int npos = 0;
   if (task < n_chunks) {
     gram_accumulate<CN, IMPLICIT, false, AccT>(col, val, chunk_begin[task], chunk_end[task], Y,
                                                ld, k, alpha, tot, bt, npos);
-    store_slot<CN, AccT>(slots + (int64_t)task * Cfg<CN>::SLOT, tot, bt, npos);
+    store_slot<NT, CN, AccT>(slots + (int64_t)task * Cfg<CN>::SLOT, tot, bt, npos);
     return;
   }
   const int row = light_rows[task - n_chunks];
@@ -597,10 +651,10 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
   double a64[NT][4], b64[CN];
-  zero_acc<CN, double>(a64, b64);
+  zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
   for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
-    add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
+    add_slot<NT, CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
   finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
                                          X + (int64_t)row * ld, ld, row, status);
@@ -613,13 +667,13 @@ __global__ __launch_bounds__(64, 2) void yty_partial_kernel(const float* __restr
                                                             double* __restrict__ slots) {
   constexpr int NT = Cfg<CN>::NT;
   double a64[NT][4], b64[CN];
-  zero_acc<CN, double>(a64, b64);
+  zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
   const int64_t pb = (int64_t)blockIdx.x * kYtyChunk;
   const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
   gram_accumulate<CN, false, true, double>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64, b64,
                                            npos);
-  store_slot<CN, double>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, npos);
+  store_slot<NT, CN, double>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, npos);
 }
 
 template <int CN>
@@ -628,13 +682,384 @@ __global__ __launch_bounds__(64) void yty_reduce_kernel(const double* __restrict
   constexpr int NT = Cfg<CN>::NT, NP = Cfg<CN>::NP;
   __shared__ double P[NP];
   double a64[NT][4], b64[CN];
-  zero_acc<CN, double>(a64, b64);
+  zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
-  for (int s = 0; s < nslots; ++s) add_slot<CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
+  for (int s = 0; s < nslots; ++s) add_slot<NT, CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
   pack_gram<CN, double>(a64, P);
   __syncthreads();
   for (int e = threadIdx.x; e < NP; e += 64) out[e] = P[e];
 }
+
+// ---------------------------------------------------------------------------
+// k in (64, 128]: one workgroup of 4 wavefronts per system (CN = 8, 36 upper
+// tiles).  Wave R accumulates the tiles of WgTiles<R> (10/10/8/8) and keeps them
+// in registers through the factorisation; the block LDL^T of tile_ldl_solve is
+// spread over the workgroup:
+//   (a) owners stage block row K (transposed) in LDS            | barrier
+//   (b) wave 0: 16x16 LDL^T of B_KK with the rhs block z_K      | barrier
+//   (c) TRSM, lane g = 64 R + lane owns column g of block row K  | barrier
+//   (d) each wave: MFMA trailing update of its own tiles (I > K)
+// and wave 0 runs the block back substitution.  (c) writes W into its own
+// buffer, so the stage may be rewritten by the next K without another barrier.
+// LDS (floats): U tiles 36*256 | stage 8*320 | W 7*256 | D, b, z, x 4*128 = 56 KB,
+// so two workgroups (8 waves, 2 per SIMD) share a CU.
+// ---------------------------------------------------------------------------
+constexpr int kWgNB = 8;
+
+struct WgLds {
+  static constexpr int NB = kWgNB, NT = NB * (NB + 1) / 2;
+  static constexpr int U = 0, S = NT * 256, W = S + NB * 320, D = W + (NB - 1) * 256,
+                       B = D + 16 * NB, Z = B + 16 * NB, X = Z + 16 * NB, SIZE = X + 16 * NB;
+};
+
+// Wave-local LDS ordering (lanes of one wave exchanging values through LDS).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <int R>
+__device__ __forceinline__ bool wg_ldl_solve(floatx4 (&A)[WgTiles<R>::N], float* __restrict__ lds,
+                                             int k, float* __restrict__ xrow, int ld) {
+  typedef WgTiles<R> TS;
+  typedef WgLds Lo;
+  constexpr int NB = kWgNB;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int i = lane & 15;
+  float* Ust = lds + Lo::U;
+  float* St = lds + Lo::S;
+  float* Wb = lds + Lo::W;
+  float* Dv = lds + Lo::D;
+  float* bv = lds + Lo::B;
+  float* zv = lds + Lo::Z;
+  float* xv = lds + Lo::X;
+  bool ok = true;
+  static_for<NB>([&](auto Kc) {
+    constexpr int K = decltype(Kc)::value;
+    // (a) stage block row K transposed: St[J-K][j][k] (row stride 20 floats)
+    static_for<TS::N>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      if constexpr (TS::g1(t) == K) {
+        constexpr int J = TS::g2(t);
+        const floatx4 v = A[t];
+        *reinterpret_cast<float4*>(St + (J - K) * 320 + m * 20 + 4 * q) =
+            make_float4(v[0], v[1], v[2], v[3]);
+      }
+    });
+    __syncthreads();
+    // (b) LDL^T of the diagonal block, rhs block as augmented column (wave 0)
+    if constexpr (R == 0) {
+      float a[16];
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const float4 v = *reinterpret_cast<const float4*>(St + i * 20 + 4 * c4);
+        a[4 * c4] = v.x; a[4 * c4 + 1] = v.y; a[4 * c4 + 2] = v.z; a[4 * c4 + 3] = v.w;
+      }
+      float bb = bv[K * 16 + i];
+      float myd = 1.f;
+#pragma unroll
+      for (int p = 0; p < 16; ++p) {
+        const float d = readlane_t(a[p], p);
+        ok = ok && (d > 0.f);
+        float u[16];
+#pragma unroll
+        for (int j = p + 1; j < 16; ++j) u[j] = readlane_t(a[p], j);
+        const float bp = readlane_t(bb, p);
+        const float l = a[p] * rcp_t(d);
+#pragma unroll
+        for (int j = p + 1; j < 16; ++j) a[j] = fmaf(-l, u[j], a[j]);
+        if (i > p) bb = fmaf(-l, bp, bb);
+        a[p] = l;
+        if (i == p) myd = d;
+      }
+      float* Lt = Ust + 256 * tile_index(NB, K, K);  // Lt[c*16 + r] = L_K[r][c]
+      if (lane < 16) {
+        Dv[K * 16 + i] = myd;
+        zv[K * 16 + i] = bb;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) Lt[c * 16 + i] = (c < i) ? a[c] : 0.f;
+      }
+    }
+    __syncthreads();
+    if constexpr (K + 1 < NB) {
+      constexpr int ncol = 16 * (NB - 1 - K);
+      // (c) TRSM: g = 64 R + lane < ncol owns column (g & 15) of block J = K+1+(g>>4)
+      if constexpr (64 * R < ncol) {
+        const int g = 64 * R + lane;
+        const bool is_col = g < ncol;
+        const int Jl = K + 1 + (is_col ? (g >> 4) : 0);
+        const float* Lt = Ust + 256 * tile_index(NB, K, K);
+        float w[16];
+        {
+          const float* src = St + (Jl - K) * 320 + i * 20;
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
+            const float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
+            w[4 * c4] = v.x; w[4 * c4 + 1] = v.y; w[4 * c4 + 2] = v.z; w[4 * c4 + 3] = v.w;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < 15; ++c) {
+          float lc[16];
+#pragma unroll
+          for (int c4 = 0; c4 < 4; ++c4) {
+            const float4 v = *reinterpret_cast<const float4*>(Lt + c * 16 + 4 * c4);
+            lc[4 * c4] = v.x; lc[4 * c4 + 1] = v.y; lc[4 * c4 + 2] = v.z; lc[4 * c4 + 3] = v.w;
+          }
+#pragma unroll
+          for (int p = c + 1; p < 16; ++p) w[p] = fmaf(-lc[p], w[c], w[p]);
+        }
+        if (is_col) {
+          float* Wd = Wb + (Jl - K - 1) * 256 + i;
+          float* Ud = Ust + 256 * tile_index(NB, K, Jl) + i;
+          float t = 0.f;
+#pragma unroll
+          for (int c = 0; c < 16; ++c) {
+            const float uc = w[c] * rcp_t(Dv[K * 16 + c]);
+            Wd[c * 16] = w[c];
+            Ud[c * 16] = uc;
+            t = fmaf(uc, zv[K * 16 + c], t);
+          }
+          bv[Jl * 16 + i] -= t;  // b_J -= U_KJ^T z_K
+        }
+      }
+      __syncthreads();
+      // (d) trailing update of this wave's tiles on the matrix cores
+      static_for<TS::N>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        constexpr int I = TS::g1(t), J = TS::g2(t);
+        if constexpr (I > K) {
+          floatx4 acc = A[t];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                -Ust[256 * tile_index(NB, K, I) + (4 * s4 + q) * 16 + m],
+                Wb[(J - K - 1) * 256 + (4 * s4 + q) * 16 + m], acc, 0, 0, 0);
+          A[t] = acc;
+        }
+      });
+    }
+  });
+  if constexpr (R == 0) {
+    // (e) block back substitution (wave 0): x_K = U_KK^-1 (D_K^-1 z_K - sum_J U_KJ x_J)
+#pragma unroll
+    for (int K = NB - 1; K >= 0; --K) {
+      float v = zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
+#pragma unroll
+      for (int J = K + 1; J < NB; ++J) {
+        const float* Ur = Ust + 256 * tile_index(NB, K, J) + i * 16;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v = fmaf(-Ur[j], xv[J * 16 + j], v);
+      }
+      const float* Lr = Ust + 256 * tile_index(NB, K, K) + i * 16;
+      float ur[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ur[j] = Lr[j];
+      float x = 0.f;
+#pragma unroll
+      for (int j = 15; j >= 0; --j) {
+        const float xj = readlane_t(v, j);
+        if (i == j) x = xj;
+        if (i < j) v = fmaf(-ur[j], xj, v);
+      }
+      if (lane < 16) xv[K * 16 + i] = x;
+      wave_lds_sync();
+    }
+    // (f) un-permute: dim d = i*8 + K  <->  xv[K*16 + i]
+    for (int d = lane; d < ld; d += 64) {
+      const float x = d < 16 * NB ? xv[(d % NB) * 16 + d / NB] : 0.f;
+      xrow[d] = (d < k && ok) ? x : 0.f;
+    }
+  }
+  return ok;
+}
+
+// Wave R's part of completing one system: rhs blocks to LDS, YtY merge (fp64,
+// then one rounding), lambda * n on the diagonal, the workgroup LDL^T.
+template <int R, bool IMPLICIT, class AccT>
+__device__ __forceinline__ void wg_finish_and_solve(AccT (&tot)[WgTiles<R>::N][4],
+                                                    AccT (&bt)[WgTiles<R>::NRA], int64_t n_reg,
+                                                    float* lds, int k, float reg,
+                                                    const double* __restrict__ yty,
+                                                    float* __restrict__ xrow, int ld, int row,
+                                                    int32_t* __restrict__ status) {
+  typedef WgTiles<R> TS;
+  constexpr int NB = kWgNB;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+#pragma unroll
+  for (int c = 0; c < TS::NR; ++c) {
+    AccT v = bt[c];
+    v += shfl_xor_t(v, 16);
+    v += shfl_xor_t(v, 32);
+    if (q == 0) lds[WgLds::B + TS::gcol(c) * 16 + m] = (float)v;
+  }
+  const float lam = (float)((double)reg * (double)n_reg);
+  floatx4 A[TS::N];
+  static_for<TS::N>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    constexpr int c1 = TS::g1(t), c2 = TS::g2(t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int i, j;
+      tile_ij<NB>(c1, c2, r, i, j);
+      float v;
+      if constexpr (IMPLICIT) {
+        const int hi = i > j ? i : j, lo = i > j ? j : i;
+        v = (float)((double)tot[t][r] + yty[hi * (hi + 1) / 2 + lo]);
+      } else {
+        v = (float)tot[t][r];
+      }
+      if (c1 == c2 && i == j) v = (i < k) ? v + lam : 1.f;
+      A[t][r] = v;
+    }
+  });
+  const bool ok = wg_ldl_solve<R>(A, lds, k, xrow, ld);
+  if (R == 0 && !ok && lane == 0) atomicCAS(status, 0, row + 1);
+}
+
+constexpr int kWgSub = Slot<10, 4>::SIZE;  // doubles per wave sub-slot (max over roles)
+constexpr int kWgSlot = 4 * kWgSub;
+
+template <int R, bool IMPLICIT>
+__device__ __forceinline__ void wg_gram_solve_task(
+    int task, const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
+    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
+    int32_t n_chunks, const float* __restrict__ Y, float* __restrict__ X, int ld, int k,
+    float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
+    int32_t* __restrict__ status, float* lds) {
+  typedef WgTiles<R> TS;
+  float tot[TS::N][4], bt[TS::NRA];
+  zero_acc<TS::N, TS::NRA, float>(tot, bt);
+  int npos = 0;
+  if (task < n_chunks) {
+    gram_accumulate<kWgNB, IMPLICIT, false, float, TS>(col, val, chunk_begin[task], chunk_end[task],
+                                                       Y, ld, k, alpha, tot, bt, npos);
+    store_slot<TS::N, TS::NRA, float>(slots + (int64_t)task * kWgSlot + R * kWgSub, tot, bt, npos);
+    return;
+  }
+  const int row = light_rows[task - n_chunks];
+  const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
+  gram_accumulate<kWgNB, IMPLICIT, false, float, TS>(col, val, pb, pe, Y, ld, k, alpha, tot, bt,
+                                                     npos);
+  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
+  wg_finish_and_solve<R, IMPLICIT, float>(tot, bt, n_reg, lds, k, reg, yty, X + (int64_t)row * ld,
+                                          ld, row, status);
+}
+
+template <int R, bool IMPLICIT>
+__device__ __forceinline__ void wg_reduce_solve_task(int h, const int64_t* __restrict__ row_ptr,
+                                                     const int32_t* __restrict__ heavy_rows,
+                                                     const int32_t* __restrict__ slot_begin,
+                                                     const double* __restrict__ slots,
+                                                     float* __restrict__ X, int ld, int k, float reg,
+                                                     const double* __restrict__ yty,
+                                                     int32_t* __restrict__ status, float* lds) {
+  typedef WgTiles<R> TS;
+  const int row = heavy_rows[h];
+  double a64[TS::N][4], b64[TS::NRA];
+  zero_acc<TS::N, TS::NRA, double>(a64, b64);
+  int npos = 0;
+  for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
+    add_slot<TS::N, TS::NRA>(slots + (int64_t)s * kWgSlot + R * kWgSub, a64, b64, npos);
+  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
+  wg_finish_and_solve<R, IMPLICIT, double>(a64, b64, n_reg, lds, k, reg, yty,
+                                           X + (int64_t)row * ld, ld, row, status);
+}
+
+template <int R>
+__device__ __forceinline__ void wg_yty_partial_task(const float* __restrict__ Y, int64_t n, int ld,
+                                                    int k, double* __restrict__ slots) {
+  typedef WgTiles<R> TS;
+  double a64[TS::N][4], b64[TS::NRA];
+  zero_acc<TS::N, TS::NRA, double>(a64, b64);
+  int npos = 0;
+  const int64_t pb = (int64_t)blockIdx.x * kYtyChunk;
+  const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
+  gram_accumulate<kWgNB, false, true, double, TS>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64,
+                                                  b64, npos);
+  store_slot<TS::N, TS::NRA, double>(slots + (int64_t)blockIdx.x * kWgSlot + R * kWgSub, a64, b64,
+                                     npos);
+}
+
+template <int R>
+__device__ __forceinline__ void wg_yty_reduce_task(const double* __restrict__ slots, int nslots,
+                                                   double* __restrict__ out) {
+  typedef WgTiles<R> TS;
+  double a64[TS::N][4], b64[TS::NRA];
+  zero_acc<TS::N, TS::NRA, double>(a64, b64);
+  int npos = 0;
+  for (int s = 0; s < nslots; ++s)
+    add_slot<TS::N, TS::NRA>(slots + (int64_t)s * kWgSlot + R * kWgSub, a64, b64, npos);
+  static_for<TS::N>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    constexpr int c1 = TS::g1(t), c2 = TS::g2(t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int i, j;
+      tile_ij<kWgNB>(c1, c2, r, i, j);
+      // a diagonal tile holds both (i, j) and (j, i): store the lower one only
+      if (c1 < c2 || i >= j) {
+        const int hi = i > j ? i : j, lo = i > j ? j : i;
+        out[hi * (hi + 1) / 2 + lo] = a64[t][r];
+      }
+    }
+  });
+}
+
+// The workgroup kernels: wave index -> role (wave-uniform branch).
+#define ALS_WG_ROLES(CALL) \
+  do {                                                                    \
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);      \
+    if (wv == 0) CALL(0);                                                 \
+    else if (wv == 1) CALL(1);                                            \
+    else if (wv == 2) CALL(2);                                            \
+    else CALL(3);                                                         \
+  } while (0)
+
+template <bool IMPLICIT>
+__global__ __launch_bounds__(256, 2) void gram_solve_wg_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
+    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
+    int32_t n_chunks, const float* __restrict__ Y, float* __restrict__ X, int ld, int k,
+    float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
+    int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
+#define CALL(R)                                                                                 \
+  wg_gram_solve_task<R, IMPLICIT>(blockIdx.x, row_ptr, col, val, light_rows, chunk_begin,      \
+                                  chunk_end, n_chunks, Y, X, ld, k, reg, alpha, yty, slots,   \
+                                  status, lds)
+  ALS_WG_ROLES(CALL);
+#undef CALL
+}
+
+template <bool IMPLICIT>
+__global__ __launch_bounds__(256, 2) void reduce_solve_wg_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
+    const int32_t* __restrict__ slot_begin, const double* __restrict__ slots,
+    float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
+    int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
+#define CALL(R)                                                                           \
+  wg_reduce_solve_task<R, IMPLICIT>(blockIdx.x, row_ptr, heavy_rows, slot_begin, slots, X, \
+                                    ld, k, reg, yty, status, lds)
+  ALS_WG_ROLES(CALL);
+#undef CALL
+}
+
+__global__ __launch_bounds__(256, 2) void yty_partial_wg_kernel(const float* __restrict__ Y,
+                                                                int64_t n, int ld, int k,
+                                                                double* __restrict__ slots) {
+#define CALL(R) wg_yty_partial_task<R>(Y, n, ld, k, slots)
+  ALS_WG_ROLES(CALL);
+#undef CALL
+}
+
+__global__ __launch_bounds__(256) void yty_reduce_wg_kernel(const double* __restrict__ slots,
+                                                            int nslots, double* __restrict__ out) {
+#define CALL(R) wg_yty_reduce_task<R>(slots, nslots, out)
+  ALS_WG_ROLES(CALL);
+#undef CALL
+}
+#undef ALS_WG_ROLES
 
 }  // namespace als
 
@@ -644,10 +1069,21 @@ extern "C" {
 
 int32_t als_k_pad(int32_t k) { return 16 * cn_for_k(k); }
 
+}  // extern "C"
+
+static size_t slot_doubles(int k) {
+  switch (cn_for_k(k)) {
+    case 1: return Cfg<1>::SLOT;
+    case 2: return Cfg<2>::SLOT;
+    case 4: return Cfg<4>::SLOT;
+    default: return kWgSlot;
+  }
+}
+
+extern "C" {
+
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks) {
-  const int cn = cn_for_k(k);
-  const size_t slot = cn == 1 ? Cfg<1>::SLOT : (cn == 2 ? Cfg<2>::SLOT : Cfg<4>::SLOT);
-  return align_up(sizeof(double) * slot * (size_t)(n_chunks > 0 ? n_chunks : 0)) + 256;
+  return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0)) + 256;
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -657,7 +1093,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const float* Y_src, float* X_dst, int32_t ld, int32_t k, float reg,
                    int implicit, float alpha, const double* yty_packed, int32_t* status_dev,
                    void* ws, size_t ws_bytes, int phases, void* stream) {
-  ALS_REQUIRE(k >= 1 && k <= 64, ALS_EUNSUPPORTED, "als_solve_half: rank %d not in [1, 64]", k);
+  ALS_REQUIRE(k >= 1 && k <= kMaxRank, ALS_EUNSUPPORTED, "als_solve_half: rank %d not in [1, %d]",
+              k, kMaxRank);
   ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_solve_half: ld=%d must be >= k and %%4==0",
               ld);
   ALS_REQUIRE(n_light >= 0 && n_heavy >= 0 && n_chunks >= 0, ALS_EINVAL,
@@ -690,29 +1127,44 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                       status_dev);                                \
     ALS_LAUNCH_CHECK();                                                                           \
   } while (0)
+#define ALS_SOLVE_WG_LAUNCH(IMP)                                                                  \
+  do {                                                                                            \
+    if (g1)                                                                                       \
+      gram_solve_wg_kernel<IMP><<<g1, 256, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,   \
+                                                    chunk_end, n_chunks, Y_src, X_dst, ld, k,     \
+                                                    reg, alpha, yty_packed, slots, status_dev);   \
+    ALS_LAUNCH_CHECK();                                                                           \
+    if (g2)                                                                                       \
+      reduce_solve_wg_kernel<IMP><<<g2, 256, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
+                                                      slots, X_dst, ld, k, reg, yty_packed,       \
+                                                      status_dev);                                \
+    ALS_LAUNCH_CHECK();                                                                           \
+  } while (0)
   if (implicit) {
     if (cn == 1) ALS_SOLVE_LAUNCH(1, true);
     else if (cn == 2) ALS_SOLVE_LAUNCH(2, true);
-    else ALS_SOLVE_LAUNCH(4, true);
+    else if (cn == 4) ALS_SOLVE_LAUNCH(4, true);
+    else ALS_SOLVE_WG_LAUNCH(true);
   } else {
     if (cn == 1) ALS_SOLVE_LAUNCH(1, false);
     else if (cn == 2) ALS_SOLVE_LAUNCH(2, false);
-    else ALS_SOLVE_LAUNCH(4, false);
+    else if (cn == 4) ALS_SOLVE_LAUNCH(4, false);
+    else ALS_SOLVE_WG_LAUNCH(false);
   }
 #undef ALS_SOLVE_LAUNCH
+#undef ALS_SOLVE_WG_LAUNCH
   return ALS_OK;
 }
 
 size_t als_yty_workspace_bytes(int64_t n, int32_t k) {
   const int64_t nslots = n > 0 ? (n + kYtyChunk - 1) / kYtyChunk : 1;
-  const int cn = cn_for_k(k);
-  const size_t slot = cn == 1 ? Cfg<1>::SLOT : (cn == 2 ? Cfg<2>::SLOT : Cfg<4>::SLOT);
-  return align_up(sizeof(double) * slot * (size_t)nslots) + 256;
+  return align_up(sizeof(double) * slot_doubles(k) * (size_t)nslots) + 256;
 }
 
 int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed_out, void* ws,
             size_t ws_bytes, void* stream) {
-  ALS_REQUIRE(k >= 1 && k <= 64, ALS_EUNSUPPORTED, "als_yty: rank %d not in [1, 64]", k);
+  ALS_REQUIRE(k >= 1 && k <= kMaxRank, ALS_EUNSUPPORTED, "als_yty: rank %d not in [1, %d]", k,
+              kMaxRank);
   ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_yty: bad ld");
   ALS_REQUIRE(n >= 0 && yty_packed_out && (n == 0 || Y), ALS_EINVAL, "als_yty: bad args");
   ALS_REQUIRE(n < (int64_t(1) << 31), ALS_EINVAL, "als_yty: n >= 2^31");
@@ -736,7 +1188,13 @@ int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed
   } while (0)
   if (cn == 1) ALS_YTY_LAUNCH(1);
   else if (cn == 2) ALS_YTY_LAUNCH(2);
-  else ALS_YTY_LAUNCH(4);
+  else if (cn == 4) ALS_YTY_LAUNCH(4);
+  else {
+    yty_partial_wg_kernel<<<nslots, 256, 0, st>>>(Y, n, ld, k, slots);
+    ALS_LAUNCH_CHECK();
+    yty_reduce_wg_kernel<<<1, 256, 0, st>>>(slots, nslots, yty_packed_out);
+    ALS_LAUNCH_CHECK();
+  }
 #undef ALS_YTY_LAUNCH
   return ALS_OK;
 }

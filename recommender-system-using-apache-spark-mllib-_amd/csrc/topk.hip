@@ -23,6 +23,7 @@ namespace als {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTopkMax = 256;
+constexpr int kLdsBytes = 160 * 1024;  // per CU on gfx950 (one workgroup may use it all)
 
 __device__ __forceinline__ bool beats(float s1, int i1, float s2, int i2) {
   return s1 > s2 || (s1 == s2 && i1 < i2);
@@ -213,7 +214,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
              void* stream) {
   (void)ws;
   (void)ws_bytes;
-  ALS_REQUIRE(k >= 1 && k <= 64, ALS_EUNSUPPORTED, "als_topk: rank %d not in [1, 64]", k);
+  ALS_REQUIRE(k >= 1 && k <= 128, ALS_EUNSUPPORTED, "als_topk: rank %d not in [1, 128]", k);
   ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_topk: bad ld");
   ALS_REQUIRE(top >= 1 && top <= kTopkMax, ALS_EUNSUPPORTED, "als_topk: top %d not in [1, %d]",
               top, kTopkMax);
@@ -222,8 +223,10 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   if (n_q == 0) return ALS_OK;
   ALS_REQUIRE(Q && V && idx_out && score_out, ALS_EINVAL, "als_topk: null pointer");
   hipStream_t st = as_stream(stream);
-  const int cn = k <= 16 ? 1 : (k <= 32 ? 2 : 4);
+  const int cn = k <= 16 ? 1 : (k <= 32 ? 2 : (k <= 64 ? 4 : 8));
   const size_t lds = topk_lds_bytes(cn, top);
+  ALS_REQUIRE(lds <= kLdsBytes, ALS_EUNSUPPORTED,
+              "als_topk: top %d at rank %d needs %zu B of LDS (> %d)", top, k, lds, kLdsBytes);
   const unsigned grid = (unsigned)((n_q + 63) / 64);
 #define ALS_TOPK_LAUNCH(CN)                                                                   \
   do {                                                                                        \
@@ -234,7 +237,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   } while (0)
   if (cn == 1) ALS_TOPK_LAUNCH(1);
   else if (cn == 2) ALS_TOPK_LAUNCH(2);
-  else ALS_TOPK_LAUNCH(4);
+  else if (cn == 4) ALS_TOPK_LAUNCH(4);
+  else ALS_TOPK_LAUNCH(8);
 #undef ALS_TOPK_LAUNCH
   return ALS_OK;
 }

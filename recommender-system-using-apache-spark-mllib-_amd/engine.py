@@ -27,6 +27,7 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 
 DEFAULT_CHUNK = 2048  # ratings per heavy-row task
+MAX_RANK = 128       # k <= 64: one wavefront per system; 64 < k <= 128: one 4-wave workgroup
 
 
 def ld_for(rank: int) -> int:
@@ -254,8 +255,8 @@ class ALSCore:
 
     # Spark ALS.initialize: unit-norm Gaussian rows, fp32.
     def init_factors(self, rank: int, seed: int = 0, U0=None) -> None:
-        if rank < 1 or rank > 64:
-            raise ValueError(f"rank must be in [1, 64] on this build, got {rank}")
+        if rank < 1 or rank > MAX_RANK:
+            raise ValueError(f"rank must be in [1, {MAX_RANK}] on this build, got {rank}")
         self.rank = rank
         ld = ld_for(rank)
         self.U = torch.zeros((self.n_users, ld), dtype=torch.float32, device=self.device)

@@ -42,8 +42,8 @@ def _validate(p: dict) -> None:
     if str(p["coldStartStrategy"]).lower() not in _COLD:
         raise ValueError(f"ALS_coldStartStrategy parameter coldStartStrategy given invalid value "
                          f"{p['coldStartStrategy']} (supported: {', '.join(_COLD)})")
-    if p["rank"] > 64:
-        raise NotImplementedError("rank > 64 is not supported by this build of the HIP kernels")
+    if p["rank"] > 128:
+        raise NotImplementedError("rank > 128 is not supported by this build of the HIP kernels")
     if p["nonnegative"]:
         raise NotImplementedError("nonnegative=True (NNLS solver) is out of scope for this build")
 

@@ -153,8 +153,8 @@ class MatrixFactorizationModel:
 def _check(rank, iterations, lambda_, nonnegative, alpha=0.0):
     if int(rank) < 1:
         raise ValueError(f"rank must be >= 1, got {rank}")
-    if int(rank) > 64:
-        raise NotImplementedError("rank > 64 is not supported by this build of the HIP kernels")
+    if int(rank) > 128:
+        raise NotImplementedError("rank > 128 is not supported by this build of the HIP kernels")
     if int(iterations) < 0:
         raise ValueError(f"iterations must be >= 0, got {iterations}")
     if lambda_ < 0:

@@ -54,9 +54,12 @@ def test_workspace_sizes_are_monotone_and_host_only():
     assert L.als_index_workspace_bytes(10, 100) < L.als_index_workspace_bytes(10, 10 ** 6)
     assert L.als_solve_workspace_bytes(64, 0) < L.als_solve_workspace_bytes(64, 100)
     assert L.als_solve_workspace_bytes(10, 100) < L.als_solve_workspace_bytes(64, 100)
+    assert L.als_solve_workspace_bytes(64, 100) < L.als_solve_workspace_bytes(128, 100)
+    assert L.als_yty_workspace_bytes(10 ** 6, 64) < L.als_yty_workspace_bytes(10 ** 6, 128)
     assert L.als_yty_workspace_bytes(10 ** 6, 64) > 0
     assert L.als_rmse_workspace_bytes(10 ** 6) > L.als_rmse_workspace_bytes(10)
-    assert [L.als_k_pad(k) for k in (1, 16, 17, 32, 33, 64)] == [16, 16, 32, 32, 64, 64]
+    assert [L.als_k_pad(k) for k in (1, 16, 17, 32, 33, 64, 65, 128)] == [16, 16, 32, 32, 64, 64,
+                                                                         128, 128]
 
 
 def _solve_args(**over):
@@ -68,7 +71,7 @@ def _solve_args(**over):
 
 
 @pytest.mark.parametrize("over,code", [
-    (dict(k=0), -4), (dict(k=65), -4), (dict(ld=62), -1), (dict(ld=32), -1),
+    (dict(k=0), -4), (dict(k=129, ld=132), -4), (dict(ld=62), -1), (dict(ld=32), -1),
     (dict(n_light=-1), -1), (dict(Y=0), -1), (dict(implicit=1), -1), (dict(reg=-1.0), -1),
     (dict(Y=18), -1), (dict(phases=0), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2)])
 def test_solve_half_argument_errors(over, code):
@@ -83,6 +86,8 @@ def test_topk_and_predict_argument_errors():
     assert L.als_topk(1, 1, 1, 1, 64, 64, 0, 1, 1, 0, 0, 0) == -4      # top = 0
     assert L.als_topk(1, 1, 1, 1, 64, 64, 257, 1, 1, 0, 0, 0) == -4    # top > 256
     assert L.als_topk(1, 1, 1, 1, 60, 64, 10, 1, 1, 0, 0, 0) == -1     # ld < k
+    assert L.als_topk(1, 1, 1, 1, 128, 128, 254, 1, 1, 0, 0, 0) == -4  # LDS > 160 KB at k=128
+    assert L.als_topk(1, 1, 1, 1, 132, 129, 10, 1, 1, 0, 0, 0) == -4   # rank > 128
     assert L.als_predict(1, 1, 5, 1, 1, 1, 1, 1, 1, 10, 0, 1, 0) == -1  # k = 0
     assert L.als_csr_build(0, 0, 0, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0) == -1
     assert L.als_index_build(0, 0, 0, 0, 0, 0, 0, 0, 0) == -1           # id_space 0

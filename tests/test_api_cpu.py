@@ -22,7 +22,7 @@ DF = pd.DataFrame({"user": [0, 1, 2], "item": [0, 1, 1], "rating": [1.0, 2.0, 3.
     (dict(rank=0), ValueError), (dict(maxIter=-1), ValueError), (dict(regParam=-0.1), ValueError),
     (dict(alpha=-1.0), ValueError), (dict(coldStartStrategy="zero"), ValueError),
     (dict(numUserBlocks=0), ValueError), (dict(nonnegative=True), NotImplementedError),
-    (dict(rank=65), NotImplementedError)])
+    (dict(rank=129), NotImplementedError)])
 def test_ml_param_validation(kw, exc):
     with pytest.raises(exc):
         MLALS(**kw).fit(DF)

@@ -77,7 +77,7 @@ def test_csr_build_bitexact(kw):
 
 
 # ---------------------------------------------------------------- K2/K3
-@pytest.mark.parametrize("rank", [1, 4, 8, 10, 12, 16, 20, 32, 48, 64])
+@pytest.mark.parametrize("rank", [1, 4, 8, 10, 12, 16, 20, 32, 48, 64, 65, 100, 128])
 @pytest.mark.parametrize("implicit", [False, True])
 def test_half_sweep_parity(rank, implicit):
     u, i, r = planted(600, 400, density=0.04, heavy_items=(7, 11), heavy_users=(5,), seed=rank,
@@ -110,7 +110,7 @@ def test_half_sweep_parity(rank, implicit):
     assert eu <= 1e-4
 
 
-@pytest.mark.parametrize("rank", [3, 16, 40, 64])
+@pytest.mark.parametrize("rank", [3, 16, 40, 64, 100, 128])
 def test_yty_parity(rank):
     rng = np.random.default_rng(rank)
     n = 20000
@@ -143,6 +143,24 @@ def test_full_fit_parity_and_rmse():
     sse, n_ref = O.rmse(U, V, umap, imap, u, i, r)
     assert n == n_ref
     assert abs(rm - math.sqrt(sse / n_ref)) <= 1e-4
+
+
+@pytest.mark.parametrize("rank,implicit,alpha", [(128, True, 40.0), (128, False, 1.0),
+                                                (72, True, 40.0)])
+def test_full_fit_parity_k128(rank, implicit, alpha):
+    """BASELINE config 3 in miniature: implicit alpha=40, rank 128, 5 iterations (the
+    4-wave workgroup path), factors vs the fp64 oracle from the same U0."""
+    u, i, r = planted(700, 450, density=0.05, seed=13, heavy_items=(4,), dup=20)
+    it, reg = 5, 0.1
+    core = _core(u, i, r, chunk=256)
+    core.init_factors(rank, seed=5)
+    U0 = core.U[:, :rank].cpu().numpy()
+    core.fit(rank, it, reg, implicit=implicit, alpha=alpha, U0=U0)
+    U, V, umap, imap, _, _ = O.train(u, i, r, rank, it, reg, implicit=implicit, alpha=alpha, U0=U0)
+    eu = rel_row_err(core.U[:, :rank].cpu().numpy(), U)
+    ev = rel_row_err(core.V[:, :rank].cpu().numpy(), V)
+    report(f"full_fit[rank={rank},implicit={implicit}]", max(eu, ev))
+    assert max(eu, ev) <= 1e-3
 
 
 # ---------------------------------------------------------------- K4
@@ -208,7 +226,7 @@ def test_compute_error_kat_on_gpu():
 
 # ---------------------------------------------------------------- K5
 @pytest.mark.parametrize("rank,top", [(4, 1), (10, 10), (32, 20), (64, 10), (64, 100),
-                                      (64, 256)])
+                                      (64, 256), (96, 10), (128, 100), (128, 253)])
 def test_topk_parity(rank, top):
     rng = np.random.default_rng(rank * 1000 + top)
     n_q, n_v = 333, 1500

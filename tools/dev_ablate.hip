@@ -26,7 +26,7 @@ __global__ __launch_bounds__(64, 2) void ablate_kernel(const int64_t* __restrict
   const int row = rows[blockIdx.x];
   const int lane = threadIdx.x;
   float tot[NT][4], bt[CN];
-  zero_acc<CN, float>(tot, bt);
+  zero_acc<NT, CN, float>(tot, bt);
   int npos = 0;
   const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
   bool gram = MODE == 0 || MODE == 1 || (MODE == 5 && (blockIdx.x & 1));

@@ -32,10 +32,15 @@ def main():
     P = ctypes.c_void_p
     L.dev_ablate.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int,
                              ctypes.c_float, P, P]
+    L.dev_ablate_wg.argtypes = L.dev_ablate.argtypes
+    wg = "--wg" in sys.argv
+    k = 128 if wg else 64
+    fn = L.dev_ablate_wg if wg else L.dev_ablate
+    modes = (0, 1, 2) if wg else (0, 1, 2, 5)
     dev = torch.device("cuda", 0)
     u, i, r = D.synthetic_config("ml25m", device=dev)
     core = E.ALSCore(u, i, r, device=dev)
-    core.init_factors(64, seed=5)
+    core.init_factors(k, seed=5)
     core.iterate(0.1)
     torch.cuda.synchronize()
     st = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -44,14 +49,14 @@ def main():
     for side, blk, Y, X in (("item", core.item_block, core.U, core.V),
                             ("user", core.user_block, core.V, core.U)):
         X2 = torch.empty_like(X)
-        for mode in (0, 1, 2, 5):
+        for mode in modes:
             times = []
             for rep in range(4):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                rc = L.dev_ablate(mode, blk.row_ptr.data_ptr(), blk.col.data_ptr(),
+                rc = fn(mode, blk.row_ptr.data_ptr(), blk.col.data_ptr(),
                                   blk.val.data_ptr(), blk.light_rows.data_ptr(), blk.n_light,
-                                  Y.data_ptr(), X2.data_ptr(), 64, 0.1, st.data_ptr(),
+                                  Y.data_ptr(), X2.data_ptr(), k, 0.1, st.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
                 e1.record()
                 torch.cuda.synchronize()

@@ -54,6 +54,63 @@ __global__ __launch_bounds__(64, 2) void ablate_kernel(const int64_t* __restrict
                                      X + (int64_t)row * ld, ld, row, status);
 }
 
+// k = 128 workgroup path (explicit), same modes 0/1/2.
+template <int R, int MODE>
+__device__ __forceinline__ void ablate_wg_task(const int64_t* __restrict__ row_ptr,
+                                               const int32_t* __restrict__ col,
+                                               const float* __restrict__ val,
+                                               const int32_t* __restrict__ rows,
+                                               const float* __restrict__ Y, float* __restrict__ X,
+                                               int ld, float reg, int32_t* __restrict__ status,
+                                               float* lds) {
+  typedef WgTiles<R> TS;
+  const int lane = threadIdx.x & 63;
+  float tot[TS::N][4], bt[TS::NRA];
+  zero_acc<TS::N, TS::NRA, float>(tot, bt);
+  int npos = 0;
+  const int row = rows[blockIdx.x];
+  const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
+  if (MODE != 2) {
+    gram_accumulate<kWgNB, false, false, float, TS>(col, val, pb, pe, Y, ld, 128, 0.f, tot, bt,
+                                                    npos);
+  } else {
+#pragma unroll
+    for (int t = 0; t < TS::N; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[t][r] = 0.01f * (float)((lane * 7 + t * 3 + r) % 11);
+    bt[0] = 1.f;
+  }
+  if (MODE == 1) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < TS::N; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s += tot[t][r];
+    for (int c = 0; c < TS::NRA; ++c) s += bt[c];
+    X[(int64_t)row * ld + (threadIdx.x & 127)] = s;
+    return;
+  }
+  wg_finish_and_solve<R, false, float>(tot, bt, (pe - pb) + 64, lds, 128, reg, nullptr,
+                                       X + (int64_t)row * ld, ld, row, status);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void ablate_wg_kernel(const int64_t* __restrict__ row_ptr,
+                                                           const int32_t* __restrict__ col,
+                                                           const float* __restrict__ val,
+                                                           const int32_t* __restrict__ rows,
+                                                           const float* __restrict__ Y,
+                                                           float* __restrict__ X, int ld,
+                                                           float reg,
+                                                           int32_t* __restrict__ status) {
+  __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wv == 0) ablate_wg_task<0, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
+  else if (wv == 1) ablate_wg_task<1, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
+  else if (wv == 2) ablate_wg_task<2, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
+  else ablate_wg_task<3, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
+}
+
 }  // namespace als
 
 extern "C" int dev_ablate(int mode, const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -67,6 +124,22 @@ extern "C" int dev_ablate(int mode, const int64_t* row_ptr, const int32_t* col, 
     case 1: L(1); break;
     case 2: L(2); break;
     case 5: L(5); break;
+    default: return -1;
+  }
+#undef L
+  return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+extern "C" int dev_ablate_wg(int mode, const int64_t* row_ptr, const int32_t* col,
+                             const float* val, const int32_t* rows, int n, const float* Y,
+                             float* X, int ld, float reg, int32_t* status, void* stream) {
+  using namespace als;
+  hipStream_t st = (hipStream_t)stream;
+#define L(M) ablate_wg_kernel<M><<<n, 256, 0, st>>>(row_ptr, col, val, rows, Y, X, ld, reg, status)
+  switch (mode) {
+    case 0: L(0); break;
+    case 1: L(1); break;
+    case 2: L(2); break;
     default: return -1;
   }
 #undef L

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 1
+#define ALS_ABI_VERSION 2
 
 #define ALS_OK 0
 #define ALS_EINVAL (-1)   /* bad argument (shape, null pointer, rank) */
@@ -94,10 +94,13 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  *   explicit:  A_j = sum_s y_s y_s^T + reg*n_j*I,          b_j = sum_s r_js y_s
  *   implicit:  A_j = YtY + sum_s c1 y_s y_s^T + reg*n+_j*I, b_j = sum_{r>0} (1+c1) y_s,
  *              c1 = alpha*|r|, n+_j = #{r_js > 0}
- * from fp32 factors (exact fp32 products on the matrix cores; fp32 sums within a
- * task of <= 2048 ratings, fp64 across a heavy row's tasks), solved by a
+ * from fp32 factors.  k <= 64: the Gram runs on the f16 matrix cores with every
+ * value split into two f16 halves (hi*hi + hi*lo + lo*hi, ~2^-21 relative per
+ * product, after a power-of-two scaling by max |Y_src| over its n_src rows, and
+ * max |rating| for implicit); 64 < k <= 128: exact fp32 products.  fp32 sums within
+ * a task of <= 2048 ratings, fp64 across a heavy row's tasks; solved by a
  * square-root-free block LDL^T (the solution of Spark's Cholesky dppsv) in fp32
- * on the matrix cores, stored fp32 into X_dst[row*ld ..].  k <= 64.
+ * on the matrix cores, stored fp32 into X_dst[row*ld ..].  k <= 128.
  * Measured against an fp64 restatement: <= 3.2e-6 relative per row (parity bar
  * 1e-4, tests/test_gpu_kernels.py).  yty_packed (implicit only): lower-packed
  * fp64 k_pad x k_pad Gram from als_yty.  status_dev: device int32, set to
@@ -112,7 +115,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* heavy_rows, const int32_t* heavy_slot_begin, int32_t n_heavy,
                    const int32_t* chunk_row, const int64_t* chunk_begin, const int64_t* chunk_end,
                    int32_t n_chunks,
-                   const float* Y_src, float* X_dst, int32_t ld, int32_t k,
+                   const float* Y_src, int64_t n_src, float* X_dst, int32_t ld, int32_t k,
                    float reg, int implicit, float alpha, const double* yty_packed,
                    int32_t* status_dev, void* ws, size_t ws_bytes, int phases, void* stream);
 

@@ -27,6 +27,7 @@
 //    as an augmented column, followed by a column-sweep back substitution.
 #include "als_common.h"
 
+#include <algorithm>
 #include <utility>
 
 namespace als {
@@ -56,6 +57,9 @@ template <int N, class F>
 __device__ __forceinline__ void static_for(F&& f) {
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
+
+// Wave-local LDS ordering (lanes of one wave exchanging values through LDS).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 template <int CN>
 __device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y)[CN]) {
@@ -265,6 +269,196 @@ __device__ __forceinline__ void gram_accumulate(const int32_t* __restrict__ col,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row Grams on the f16 matrix cores with fp32-grade products ("split" Gram).
+//
+// v_mfma_f32_16x16x4_f32 runs at the fp32 VECTOR rate on gfx950 and occupies
+// the VALU issue port, so an fp32-MFMA Gram leaves nothing for the solves of
+// the other waves.  Here every gathered value t = w*y (w = per-launch power-of-
+// two scale, times sqrt(alpha |r|) for implicit) is split into
+//   t = hi + lo,  hi = f16_rn(t),  lo = f16_rn(t - hi)   (~22 significant bits)
+// and the Gram tile is  sum hi_a hi_b + hi_a lo_b + lo_a hi_b  — three
+// v_mfma_f32_16x16x32_f16 per tile per 32 ratings (16x the fp32-MFMA rate,
+// so 5.3x fewer matrix cycles), exact f16 products accumulated in fp32.  The
+// dropped lo*lo term and the two roundings are ~2^-21 relative per product:
+// the Gram matches an fp32 one to within its own accumulation error.
+// The scale keeps |t| in [2^14, 2^15) for the largest entry, so hi never
+// overflows and lo stays normal for entries within ~2^17 of the largest.
+// MFMA K dimension = rating index: lane (q, m) holds ratings 8q..8q+7 of a
+// 32-rating step and dims m*CN .. m*CN+CN-1, exactly the dim permutation of
+// the fp32 path, so the C layout (and the solve that consumes it) is unchanged.
+// rhs b = sum coef * y stays an fp32 VALU FMA on the unscaled values.
+// ---------------------------------------------------------------------------
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half8v __attribute__((ext_vector_type(8)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+
+// Round-to-nearest packed conversions (v_cvt_pk_f16_f32): unbiased pieces; the
+// residual t - hi is exact in fp32.
+__device__ __forceinline__ void split_pair(float t0, float t1, uint32_t& hi, uint32_t& lo) {
+  const half2v h = __builtin_convertvector((float2v){t0, t1}, half2v);
+  const half2v l = __builtin_convertvector((float2v){t0 - (float)h[0], t1 - (float)h[1]}, half2v);
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
+__device__ __forceinline__ half8v as_h8(const uint32_t (&v)[4]) {
+  return __builtin_bit_cast(half8v, make_uint4(v[0], v[1], v[2], v[3]));
+}
+
+// Power-of-two scale for the split: the largest |w y| lands in [2^14, 2^15).
+__device__ __forceinline__ int split_exponent(float m) {
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+  int e = 14 - ilogbf(m);
+  return e < -60 ? -60 : (e > 60 ? 60 : e);
+}
+
+// Per-step register set of the split Gram: 8 ratings x NC dims of this lane
+// (unscaled), their ratings, and validity via y = 0.
+template <int NC>
+struct SplitStep {
+  float y[8][NC];
+  float r[8];
+};
+
+// Stage the (column, rating) pairs of one 64-rating block in LDS (wave-private).
+__device__ __forceinline__ void stage_block(int* __restrict__ st_c, float* __restrict__ st_r, int ci,
+                                            float rv) {
+  const int lane = threadIdx.x & 63;
+  st_c[lane] = ci;
+  st_r[lane] = rv;
+}
+
+// Issue the gathers of one 32-rating step (half h of the staged block).
+template <int CN, class TS>
+__device__ __forceinline__ void split_issue(SplitStep<TS::NC>& s, const int* __restrict__ st_c,
+                                            const float* __restrict__ st_r, int h,
+                                            const float* __restrict__ Y, int ld, int d0, int k) {
+  const int q = (threadIdx.x & 63) >> 4;
+  const int o = 32 * h + 8 * q;
+  const int4 c0 = *reinterpret_cast<const int4*>(st_c + o);
+  const int4 c1 = *reinterpret_cast<const int4*>(st_c + o + 4);
+  const float4 r0 = *reinterpret_cast<const float4*>(st_r + o);
+  const float4 r1 = *reinterpret_cast<const float4*>(st_r + o + 4);
+  const int ids[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  s.r[0] = r0.x; s.r[1] = r0.y; s.r[2] = r0.z; s.r[3] = r0.w;
+  s.r[4] = r1.x; s.r[5] = r1.y; s.r[6] = r1.z; s.r[7] = r1.w;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (ids[j] >= 0) {
+      TS::load(Y + (int64_t)ids[j] * ld + d0, s.y[j], d0, k);
+    } else {
+#pragma unroll
+      for (int c = 0; c < TS::NC; ++c) s.y[j][c] = 0.f;
+    }
+  }
+}
+
+// Consume one step: rhs FMAs, split, 3 f16 MFMAs per tile.
+template <class TS, bool IMPLICIT>
+__device__ __forceinline__ void split_consume(const SplitStep<TS::NC>& s, float sc, float alpha,
+                                              floatx4 (&acc)[TS::N], float (&bf)[TS::NRA]) {
+  float w[8], cb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if constexpr (IMPLICIT) {
+      const float c1 = alpha * fabsf(s.r[j]);
+      w[j] = sc * __builtin_sqrtf(c1);
+      cb[j] = s.r[j] > 0.f ? 1.f + c1 : 0.f;
+    } else {
+      w[j] = sc;
+      cb[j] = s.r[j];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < TS::NR; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[c] = fmaf(cb[j], s.y[j][c], bf[c]);
+  uint32_t hi[TS::NC][4], lo[TS::NC][4];
+#pragma unroll
+  for (int c = 0; c < TS::NC; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      split_pair(w[2 * p] * s.y[2 * p][c], w[2 * p + 1] * s.y[2 * p + 1][c], hi[c][p], lo[c][p]);
+  static_for<TS::N>([&](auto ti) {
+    constexpr int tt = decltype(ti)::value;
+    constexpr int a = TS::l1(tt), b = TS::l2(tt);
+    const half8v ha = as_h8(hi[a]), hb = as_h8(hi[b]);
+    acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[tt], 0, 0, 0);
+    acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, as_h8(lo[b]), acc[tt], 0, 0, 0);
+    acc[tt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(lo[a]), hb, acc[tt], 0, 0, 0);
+  });
+}
+
+// Gram + rhs of ratings [pb, pe) of one row with the split f16 MFMA.
+// acc: scaled Gram tiles (x sc^2), bf: per-lane partial rhs (unscaled, summed
+// over the 4 rating slots q by the caller), npos: #ratings > 0 (implicit).
+// Pipeline: the gathers of step s+1 are in flight while step s is consumed;
+// the (column, rating) pairs of the next 64-block are prefetched into registers
+// and staged in LDS (`st`, 128 words, wave-private) when that block starts.
+template <int CN, bool IMPLICIT, class TS = FullTiles<CN>>
+__device__ __forceinline__ void gram_accumulate_split(
+    const int32_t* __restrict__ col, const float* __restrict__ val, int64_t pb, int64_t pe,
+    const float* __restrict__ Y, int ld, int k, float alpha, float sc,
+    floatx4 (&acc)[TS::N], float (&bf)[TS::NRA], int& npos, int* __restrict__ st) {
+  const int lane = threadIdx.x & 63, m = lane & 15;
+  const int d0 = m * CN;
+  int* st_c = st;
+  float* st_r = reinterpret_cast<float*>(st + 64);
+  if (pe <= pb) return;
+  auto load_idx = [&](int64_t base, int& ci, float& rv) {
+    ci = -1;
+    rv = 0.f;
+    if (base + lane < pe) {
+      ci = col[base + lane];
+      rv = val[base + lane];
+    }
+  };
+  const int64_t n = pe - pb;
+  const int nsteps = (int)((n + 31) >> 5);
+  int ci_n, ci_c;
+  float rv_n, rv_c;
+  load_idx(pb, ci_c, rv_c);
+  load_idx(pb + 64, ci_n, rv_n);
+  stage_block(st_c, st_r, ci_c, rv_c);
+  if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_c >= 0 && rv_c > 0.f));
+  wave_lds_sync();
+  SplitStep<TS::NC> sA, sB;
+  split_issue<CN, TS>(sA, st_c, st_r, 0, Y, ld, d0, k);
+  // step s uses block s>>1, half s&1; before issuing step s+1 = 2b+2 the block
+  // b+1 is staged (its pairs were prefetched into ci_n/rv_n one block earlier).
+  auto next = [&](SplitStep<TS::NC>& dst, int s1) {
+    if ((s1 & 1) == 0) {
+      stage_block(st_c, st_r, ci_n, rv_n);
+      if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_n >= 0 && rv_n > 0.f));
+      wave_lds_sync();
+      load_idx(pb + 64 * (int64_t)((s1 >> 1) + 1), ci_n, rv_n);
+    }
+    split_issue<CN, TS>(dst, st_c, st_r, s1 & 1, Y, ld, d0, k);
+  };
+  // rhs: 16-term fp32 partials per lane and 64-rating block, summed into bf
+  float bp[TS::NRA];
+  auto flush = [&]() {
+#pragma unroll
+    for (int c = 0; c < TS::NRA; ++c) {
+      bf[c] += bp[c];
+      bp[c] = 0.f;
+    }
+  };
+#pragma unroll
+  for (int c = 0; c < TS::NRA; ++c) bp[c] = 0.f;
+  int s = 0;
+  for (; s + 2 <= nsteps; s += 2) {
+    next(sB, s + 1);
+    split_consume<TS, IMPLICIT>(sA, sc, alpha, acc, bp);
+    if (s + 2 < nsteps) next(sA, s + 2);
+    split_consume<TS, IMPLICIT>(sB, sc, alpha, acc, bp);
+    flush();
+  }
+  if (s < nsteps) split_consume<TS, IMPLICIT>(sA, sc, alpha, acc, bp);
+  flush();
+}
+
 // (i, j) of register r of upper tile tt for this lane (MFMA 16x16 C layout:
 // row = 4q + r, col = m; dims interleaved as d = 16-index * CN + tile-index).
 template <int CN>
@@ -306,28 +500,32 @@ __device__ __forceinline__ float readlane_t(float v, int l) {
 __device__ __forceinline__ double readlane_t(double v, int l) { return readlane_f64(v, l); }
 
 // ---------------------------------------------------------------------------
-// Block LDL^T on the matrix cores.
+// Block LDL^T on a column-per-lane panel (k <= 64, one wavefront per system).
 //
 // The regularised Gram arrives as fp32 16x16 tiles in the MFMA C layout
-// (A[t] = tile (I, J), I <= J; dims permuted so that block I holds the dims
-// d = 16-index * CN + I).  Any symmetric permutation is a valid pivot order, so
-// the matrix is factored as A = U^T D U (U unit upper) in that block order:
-//   for K: factor B_KK = U_KK^T D_K U_KK and forward-solve the rhs block
-//                                                    (16x16, row per lane, v_readlane broadcasts)
-//          W_KJ = U_KK^-T B_KJ, U_KJ = D_K^-1 W_KJ     (TRSM, one lane per column)
-//          B_IJ -= U_KI^T W_KJ   for K < I <= J        (v_mfma_f32_16x16x4_f32, 4 per tile)
-//          b_J  -= U_KJ^T z_K                          (TRSM lanes)
-// then a block back substitution x_K = U_KK^-1 (D_K^-1 z_K - sum_J U_KJ x_J).
-// The O(k^3) trailing work runs on the MFMA pipe; the VALU keeps only the
-// 16-wide diagonal factorisations and TRSMs.
-// LDS (floats): U tiles NT*256 (diagonal slots: column-major L_K) |
-// stage/W NB*320 | D, b, z, x 4*16*NB.
+// (A[t] = tile (I, J), I <= J; block I holds dims d = 16-index * CN + I).  Any
+// symmetric permutation is a valid pivot order, so A = U^T D U (U unit upper)
+// is factored in that block order.  For block row K, lane t holds column t of
+// the 16 x 16(NB-K) panel [B_KK | B_K,K+1 | ...] (16 registers) plus one rhs
+// value (b of the dim that column stands for).  Because B_KK is symmetric, its
+// columns are its rows, and the 16-pivot elimination of the diagonal block, the
+// TRSM of the off-diagonal panel (W = L^-1 B) and the forward substitution of
+// the rhs — including the rhs trailing update b_J -= U_KJ^T D z_K — are ONE
+// instruction stream over all lanes:
+//   pivot p: d = R_p[p], f_t = R_t[p] / d (= U[p][t]),
+//            R_t[i] -= R_p[i] * f_t (i > p),  rb_t -= f_t * rb_p
+// (R_p[i] and rb_p broadcast from lane p by v_readlane).  The trailing tiles
+// B_IJ -= U_KI^T D_K U_KJ (K < I <= J) run on the matrix cores from the U
+// columns in LDS.  Back substitution x_K = U_KK^-1 (z_K / D_K - sum_J U_KJ x_J)
+// on 16 lanes (DPP row broadcasts).
+// LDS (floats): tile slots NT x 320 (16 columns, stride 20: conflict-free MFMA
+// operand reads) | z, d, x 3 x 16 NB.
 // ---------------------------------------------------------------------------
 template <int CN>
-struct TileLds {
-  static constexpr int NB = CN, NT = CN * (CN + 1) / 2;
-  static constexpr int U = 0, S = NT * 256, D = S + NB * 320, B = D + 16 * NB,
-                       Z = B + 16 * NB, X = Z + 16 * NB, SIZE = X + 16 * NB;
+struct PanelLds {
+  static constexpr int NB = CN, NT = CN * (CN + 1) / 2, CS = 20;  // column stride
+  static constexpr int T = 0, Z = NT * 16 * CS, D = Z + 16 * NB, X = D + 16 * NB,
+                       SIZE = X + 16 * NB;
 };
 
 __host__ __device__ constexpr int tile_index(int nb, int i, int j) {
@@ -356,154 +554,131 @@ __device__ __forceinline__ void regularise_f32(floatx4 (&A)[Cfg<CN>::NT], float 
   }
 }
 
+template <int P>
+__device__ __forceinline__ float newbcast(float v) {  // lane P of each 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                                0x150 + P, 0xF, 0xF, false));
+}
+
 template <int CN>
-__device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const float (&bq)[CN],
-                                               float* __restrict__ lds, int k,
-                                               float* __restrict__ xrow, int ld) {
-  typedef TileLds<CN> Lo;
-  constexpr int NB = CN;
+__device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const float (&bq)[CN],
+                                                float* __restrict__ lds, int k,
+                                                float* __restrict__ xrow, int ld) {
+  typedef PanelLds<CN> Lo;
+  constexpr int NB = CN, CS = Lo::CS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  const int i = lane & 15;  // row owned in the 16-wide steps (lanes >= 16 mirror)
-  float* Ust = lds + Lo::U;
-  float* St = lds + Lo::S;
+  float* Zv = lds + Lo::Z;
   float* Dv = lds + Lo::D;
-  float* bv = lds + Lo::B;
-  float* zv = lds + Lo::Z;
-  float* xv = lds + Lo::X;
-  if (q == 0) {
+  float* Xv = lds + Lo::X;
+  auto slot = [&](int I, int J) { return lds + Lo::T + tile_index(NB, I, J) * 16 * CS; };
+  // rhs of this lane's panel column at K = 0: dim m*CN + (block q)
+  float rb = 0.f;
 #pragma unroll
-    for (int c = 0; c < CN; ++c) bv[c * 16 + m] = bq[c];
-  }
+  for (int c = 0; c < CN; ++c)
+    if (q == c) rb = bq[c];
   bool ok = true;
-#pragma unroll
-  for (int K = 0; K < NB; ++K) {
-    // (a) stage block row K transposed: St[J-K][j][k] (row stride 20 floats)
-#pragma unroll
-    for (int J = K; J < NB; ++J) {
+  static_for<NB>([&](auto Kc) {
+    constexpr int K = decltype(Kc)::value;
+    constexpr int NCOL = 16 * (NB - K);
+    // (a) block row K: C layout -> column-major tile slots (column m, rows 4q..4q+3)
+    static_for<NB - K>([&](auto jc) {
+      constexpr int J = K + decltype(jc)::value;
       const floatx4 v = A[tile_index(NB, K, J)];
-      *reinterpret_cast<float4*>(St + (J - K) * 320 + m * 20 + 4 * q) =
-          make_float4(v[0], v[1], v[2], v[3]);
-    }
-    __syncthreads();
-    // (b) LDL^T of the diagonal block with the rhs block as augmented column.
-    float a[16];
+      *reinterpret_cast<float4*>(slot(K, J) + m * CS + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+    });
+    wave_lds_sync();
+    const bool col_ok = lane < NCOL;
+    const int Jl = K + (col_ok ? q : 0);
+    float* colp = slot(K, Jl) + m * CS;
+    float R[16];
 #pragma unroll
     for (int c4 = 0; c4 < 4; ++c4) {
-      const float4 v = *reinterpret_cast<const float4*>(St + i * 20 + 4 * c4);
-      a[4 * c4] = v.x; a[4 * c4 + 1] = v.y; a[4 * c4 + 2] = v.z; a[4 * c4 + 3] = v.w;
+      const float4 v = *reinterpret_cast<const float4*>(colp + 4 * c4);
+      R[4 * c4] = v.x; R[4 * c4 + 1] = v.y; R[4 * c4 + 2] = v.z; R[4 * c4 + 3] = v.w;
     }
-    float bb = bv[K * 16 + i];
+    // (b) 16 pivots over the whole panel (diag LDL^T + TRSM + rhs forward)
     float myd = 1.f;
 #pragma unroll
     for (int p = 0; p < 16; ++p) {
-      const float d = readlane_t(a[p], p);
+      const float d = readlane_t(R[p], p);
       ok = ok && (d > 0.f);
-      float u[16];
+      const float rd = rcp_t(d);
+      const float bp = readlane_t(rb, p);
+      const float f = lane > p ? R[p] * rd : 0.f;  // U[p][t]; 0 below the diagonal
+      rb = fmaf(-f, bp, rb);
 #pragma unroll
-      for (int j = p + 1; j < 16; ++j) u[j] = readlane_t(a[p], j);  // A'[j][p]
-      const float bp = readlane_t(bb, p);
-      const float l = a[p] * rcp_t(d);                                 // L[i][p]
-#pragma unroll
-      for (int j = p + 1; j < 16; ++j) a[j] = fmaf(-l, u[j], a[j]);
-      if (i > p) bb = fmaf(-l, bp, bb);
-      a[p] = l;
-      if (i == p) myd = d;
+      for (int i = p + 1; i < 16; ++i) R[i] = fmaf(-readlane_t(R[i], p), f, R[i]);
+      R[p] = f;
+      if (lane == p) myd = d;
     }
-    float* Lt = Ust + 256 * tile_index(NB, K, K);  // Lt[c*16 + r] = L_K[r][c]
+    // (c) U columns -> tile slots (block row K); z_K, D_K
+    if (col_ok) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        *reinterpret_cast<float4*>(colp + 4 * c4) =
+            make_float4(R[4 * c4], R[4 * c4 + 1], R[4 * c4 + 2], R[4 * c4 + 3]);
+    }
     if (lane < 16) {
-      Dv[K * 16 + i] = myd;
-      zv[K * 16 + i] = bb;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) Lt[c * 16 + i] = (c < i) ? a[c] : 0.f;
+      Zv[K * 16 + lane] = rb;
+      Dv[K * 16 + lane] = myd;
     }
-    __syncthreads();
-    if (K + 1 < NB) {
-      // (c) TRSM: lane t < 16*(NB-1-K) owns column (t&15) of block J = K+1+(t>>4).
-      const int ncol = 16 * (NB - 1 - K);
-      const int Jl = K + 1 + (lane >> 4);
-      const bool is_col = lane < ncol;
-      float w[16];
-      {
-        const float* src = St + (is_col ? (Jl - K) : 1) * 320 + i * 20;
+    if constexpr (K + 1 < NB) {
+      rb = __shfl(rb, (lane + 16) & 63);  // next block row's rhs: columns shift by 16
+      wave_lds_sync();
+      // (d) trailing update B_IJ -= (D_K U_KI)^T U_KJ on the matrix cores
+      float dq[4];
 #pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          const float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
-          w[4 * c4] = v.x; w[4 * c4 + 1] = v.y; w[4 * c4 + 2] = v.z; w[4 * c4 + 3] = v.w;
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 15; ++c) {
-        float lc[16];
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4) {
-          const float4 v = *reinterpret_cast<const float4*>(Lt + c * 16 + 4 * c4);
-          lc[4 * c4] = v.x; lc[4 * c4 + 1] = v.y; lc[4 * c4 + 2] = v.z; lc[4 * c4 + 3] = v.w;
-        }
-#pragma unroll
-        for (int p = c + 1; p < 16; ++p) w[p] = fmaf(-lc[p], w[c], w[p]);
-      }
-      __syncthreads();  // all stage reads done before W overwrites the stage
-      if (is_col) {
-        float* Wd = St + (Jl - K - 1) * 256 + i;
-        float* Ud = Ust + 256 * tile_index(NB, K, Jl) + i;
-        float t = 0.f;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const float uc = w[c] * rcp_t(Dv[K * 16 + c]);
-          Wd[c * 16] = w[c];
-          Ud[c * 16] = uc;
-          t = fmaf(uc, zv[K * 16 + c], t);
-        }
-        bv[Jl * 16 + i] -= t;  // rhs trailing update b_J -= U_KJ^T z_K
-      }
-      __syncthreads();
-      // (d) trailing update on the matrix cores
-#pragma unroll
-      for (int I = K + 1; I < NB; ++I) {
+      for (int s4 = 0; s4 < 4; ++s4) dq[s4] = -Dv[K * 16 + 4 * s4 + q];
+      static_for<NB - 1 - K>([&](auto ic) {
+        constexpr int I = K + 1 + decltype(ic)::value;
         float ua[4];
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          ua[s4] = -Ust[256 * tile_index(NB, K, I) + (4 * s4 + q) * 16 + m];
-#pragma unroll
-        for (int J = I; J < NB; ++J) {
+        for (int s4 = 0; s4 < 4; ++s4) ua[s4] = dq[s4] * slot(K, I)[m * CS + 4 * s4 + q];
+        static_for<NB - I>([&](auto jc) {
+          constexpr int J = I + decltype(jc)::value;
           floatx4 acc = A[tile_index(NB, I, J)];
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                ua[s4], St[(J - K - 1) * 256 + (4 * s4 + q) * 16 + m], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ua[s4], slot(K, J)[m * CS + 4 * s4 + q],
+                                                        acc, 0, 0, 0);
           A[tile_index(NB, I, J)] = acc;
-        }
+        });
+      });
+    }
+  });
+  wave_lds_sync();
+  // (e) back substitution on lanes 0..15 (lanes 16.. mirror): U_KK columns hold 0
+  // on and below the diagonal, so no masks are needed.
+  const int i = m;
+  static_for<NB>([&](auto kr) {
+    constexpr int K = NB - 1 - decltype(kr)::value;
+    float v = Zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
+    static_for<NB - 1 - K>([&](auto jc) {
+      constexpr int J = K + 1 + decltype(jc)::value;
+      const float* U = slot(K, J);
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const float4 xj = *reinterpret_cast<const float4*>(Xv + J * 16 + 4 * j4);
+        v = fmaf(-U[(4 * j4 + 0) * CS + i], xj.x, v);
+        v = fmaf(-U[(4 * j4 + 1) * CS + i], xj.y, v);
+        v = fmaf(-U[(4 * j4 + 2) * CS + i], xj.z, v);
+        v = fmaf(-U[(4 * j4 + 3) * CS + i], xj.w, v);
       }
-      __syncthreads();
-    }
-  }
-  // (e) block back substitution: x_K = U_KK^-1 (D_K^-1 z_K - sum_{J>K} U_KJ x_J)
+    });
+    const float* Ukk = slot(K, K);
+    float u[16];
 #pragma unroll
-  for (int K = NB - 1; K >= 0; --K) {
-    float v = zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
-#pragma unroll
-    for (int J = K + 1; J < NB; ++J) {
-      const float* Ur = Ust + 256 * tile_index(NB, K, J) + i * 16;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v = fmaf(-Ur[j], xv[J * 16 + j], v);
-    }
-    const float* Lr = Ust + 256 * tile_index(NB, K, K) + i * 16;  // U_KK[i][j] = L_K[j][i]
-    float ur[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) ur[j] = Lr[j];
-    float x = 0.f;
-#pragma unroll
-    for (int j = 15; j >= 0; --j) {
-      const float xj = readlane_t(v, j);
-      if (i == j) x = xj;
-      if (i < j) v = fmaf(-ur[j], xj, v);
-    }
-    if (lane < 16) xv[K * 16 + i] = x;
-    __syncthreads();
-  }
-  // (f) un-permute: dim d = i*CN + K  <->  xv[K*16 + i]
+    for (int j = 0; j < 16; ++j) u[j] = Ukk[j * CS + i];
+    static_for<16>([&](auto jr) {
+      constexpr int j = 15 - decltype(jr)::value;
+      v = fmaf(-u[j], newbcast<j>(v), v);
+    });
+    if (lane < 16) Xv[K * 16 + i] = v;
+    wave_lds_sync();
+  });
+  // (f) un-permute: dim d = i*CN + K  <->  Xv[K*16 + i]
   for (int d = lane; d < ld; d += 64) {
-    const float x = d < 16 * CN ? xv[(d % CN) * 16 + d / CN] : 0.f;
+    const float x = d < 16 * CN ? Xv[(d % CN) * 16 + d / CN] : 0.f;
     xrow[d] = (d < k && ok) ? x : 0.f;
   }
   return ok;
@@ -511,7 +686,7 @@ __device__ __forceinline__ bool tile_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const 
 
 template <int CN>
 struct SmemBytes {
-  static constexpr int value = (int)sizeof(float) * TileLds<CN>::SIZE;
+  static constexpr int value = (int)sizeof(float) * PanelLds<CN>::SIZE;
 };
 
 __device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
@@ -559,7 +734,7 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
     }
   }
   regularise_f32<CN>(A, (float)((double)reg * (double)n_reg), k);
-  const bool ok = tile_ldl_solve<CN>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  const bool ok = panel_ldl_solve<CN>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
   if (!ok && (threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -608,8 +783,9 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 
 // Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) first,
 // then whole light rows (Gram + solve fused, A never leaves the CU).
-// Per-task Gram sums in fp32 (<= 2048 ratings: 64-rating exact-product MFMA
-// blocks summed in fp32), cross-chunk sums of heavy rows in fp64.
+// Gram on the split f16 MFMA (gram_accumulate_split), fp32 accumulation over a
+// task (<= chunk ratings), fp64 across the chunks of a heavy row.
+// scal[0] = max |Y| (als_absmax_kernel), scal[1] = max |rating| (implicit).
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -617,26 +793,82 @@ __global__ __launch_bounds__(64, 2) void gram_solve_kernel(
     const int32_t* __restrict__ chunk_row, const int64_t* __restrict__ chunk_begin,
     const int64_t* __restrict__ chunk_end, int32_t n_chunks, const float* __restrict__ Y,
     float* __restrict__ X, int ld, int k, float reg, float alpha,
-    const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status) {
+    const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status,
+    const float* __restrict__ scal) {
   constexpr int NT = Cfg<CN>::NT;
-  typedef float AccT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int task = blockIdx.x;
-  AccT tot[NT][4], bt[CN];
-  zero_acc<NT, CN, AccT>(tot, bt);
+  const float wmax = IMPLICIT ? __builtin_sqrtf(alpha * scal[1]) : 1.f;
+  const int e = split_exponent(scal[0] * wmax);
+  const float sc = ldexpf(1.f, e), inv2 = ldexpf(1.f, -2 * e);
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float tot[NT][4], bt[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) bt[c] = 0.f;
   int npos = 0;
+  int64_t pb, pe;
+  int row = -1;
   if (task < n_chunks) {
-    gram_accumulate<CN, IMPLICIT, false, AccT>(col, val, chunk_begin[task], chunk_end[task], Y,
-                                               ld, k, alpha, tot, bt, npos);
-    store_slot<NT, CN, AccT>(slots + (int64_t)task * Cfg<CN>::SLOT, tot, bt, npos);
+    pb = chunk_begin[task];
+    pe = chunk_end[task];
+  } else {
+    row = light_rows[task - n_chunks];
+    pb = row_ptr[row];
+    pe = row_ptr[row + 1];
+  }
+  gram_accumulate_split<CN, IMPLICIT>(col, val, pb, pe, Y, ld, k, alpha, sc, acc, bt, npos,
+                                      reinterpret_cast<int*>(smem));
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
+  if (task < n_chunks) {
+    store_slot<NT, CN, float>(slots + (int64_t)task * Cfg<CN>::SLOT, tot, bt, npos);
     return;
   }
-  const int row = light_rows[task - n_chunks];
-  const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
-  gram_accumulate<CN, IMPLICIT, false, AccT>(col, val, pb, pe, Y, ld, k, alpha, tot, bt, npos);
+  __syncthreads();  // staging area is reused by the solve
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  finish_and_solve<CN, IMPLICIT, AccT>(tot, bt, n_reg, smem, k, reg, yty, X + (int64_t)row * ld,
-                                       ld, row, status);
+  finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty, X + (int64_t)row * ld,
+                                        ld, row, status);
+}
+
+__device__ __forceinline__ void block_absmax_publish(float m, unsigned* __restrict__ out) {
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(out, __float_as_uint(m));  // NaN-free non-negative floats order as uints
+  }
+}
+
+// max |rating| of a CSR block (ratings val[0, row_ptr[n_rows])) -> *out.
+__global__ __launch_bounds__(256) void absmax_csr_kernel(const int64_t* __restrict__ row_ptr,
+                                                         int32_t n_rows,
+                                                         const float* __restrict__ val,
+                                                         unsigned* __restrict__ out) {
+  const int64_t n = row_ptr[n_rows];
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf(val[i]));
+  block_absmax_publish(m, out);
+}
+
+// max |x| over n floats -> *out (as ordered uint bits; *out zeroed beforehand).
+__global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t n,
+                                                     unsigned* __restrict__ out) {
+  float m = 0.f;
+  const int64_t n4 = n >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = x4[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = fmaxf(m, fabsf(x[4 * n4 + threadIdx.x]));
+  block_absmax_publish(m, out);
 }
 
 // Launch 2: heavy rows — sum their chunk slots in a fixed order (fp64), then solve.
@@ -712,8 +944,6 @@ struct WgLds {
                        B = D + 16 * NB, Z = B + 16 * NB, X = Z + 16 * NB, SIZE = X + 16 * NB;
 };
 
-// Wave-local LDS ordering (lanes of one wave exchanging values through LDS).
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 template <int R>
 __device__ __forceinline__ bool wg_ldl_solve(floatx4 (&A)[WgTiles<R>::N], float* __restrict__ lds,
@@ -1083,6 +1313,7 @@ static size_t slot_doubles(int k) {
 extern "C" {
 
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks) {
+  // partial slots of the heavy-row chunks, then 256 B of scale words
   return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0)) + 256;
 }
 
@@ -1090,9 +1321,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light, const int32_t* heavy_rows,
                    const int32_t* heavy_slot_begin, int32_t n_heavy, const int32_t* chunk_row,
                    const int64_t* chunk_begin, const int64_t* chunk_end, int32_t n_chunks,
-                   const float* Y_src, float* X_dst, int32_t ld, int32_t k, float reg,
-                   int implicit, float alpha, const double* yty_packed, int32_t* status_dev,
-                   void* ws, size_t ws_bytes, int phases, void* stream) {
+                   const float* Y_src, int64_t n_src, float* X_dst, int32_t ld, int32_t k,
+                   float reg, int implicit, float alpha, const double* yty_packed,
+                   int32_t* status_dev, void* ws, size_t ws_bytes, int phases, void* stream) {
   ALS_REQUIRE(k >= 1 && k <= kMaxRank, ALS_EUNSUPPORTED, "als_solve_half: rank %d not in [1, %d]",
               k, kMaxRank);
   ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_solve_half: ld=%d must be >= k and %%4==0",
@@ -1107,10 +1338,31 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks), ALS_EWORKSPACE,
               "als_solve_half: workspace %zu < %zu", ws_bytes,
               als_solve_workspace_bytes(k, n_chunks));
+  ALS_REQUIRE(n_src >= 0, ALS_EINVAL, "als_solve_half: n_src < 0");
   hipStream_t st = as_stream(stream);
   double* slots = static_cast<double*>(ws);
+  // scale words (max |Y_src|, max |rating|) after the partial slots
+  unsigned* scal_u = reinterpret_cast<unsigned*>(static_cast<char*>(ws) +
+                                                 align_up(sizeof(double) * slot_doubles(k) *
+                                                          (size_t)(n_chunks > 0 ? n_chunks : 0)));
+  const float* scal = reinterpret_cast<const float*>(scal_u);
   const int cn = cn_for_k(k);
   ALS_REQUIRE(phases >= 1 && phases <= 3, ALS_EINVAL, "als_solve_half: phases must be 1, 2 or 3");
+  if ((phases & 1) && n_chunks + n_light > 0 && cn <= 4) {
+    ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
+    const int64_t ny = n_src * (int64_t)ld;
+    if (ny > 0) {
+      const int gy = (int)std::min<int64_t>(1024, (ny / 4 + 255) / 256 + 1);
+      absmax_kernel<<<gy, 256, 0, st>>>(Y_src, ny, scal_u);
+      ALS_LAUNCH_CHECK();
+    }
+    if (implicit) {
+      ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
+      // every row is light or heavy: the block's ratings are val[0, row_ptr[n_light + n_heavy])
+      absmax_csr_kernel<<<1024, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
+      ALS_LAUNCH_CHECK();
+    }
+  }
   const unsigned g1 = (phases & 1) ? (unsigned)(n_chunks + n_light) : 0u;
   const unsigned g2 = (phases & 2) ? (unsigned)n_heavy : 0u;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
@@ -1119,7 +1371,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
                                                     chunk_begin, chunk_end, n_chunks, Y_src,      \
                                                     X_dst, ld, k, reg, alpha, yty_packed, slots,  \
-                                                    status_dev);                                  \
+                                                    status_dev, scal);                            \
     ALS_LAUNCH_CHECK();                                                                           \
     if (g2)                                                                                       \
       reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \

@@ -173,7 +173,8 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
                            ptr(block.light_rows), block.n_light, ptr(block.heavy_rows),
                            ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),
                            ptr(block.chunk_begin), ptr(block.chunk_end), block.n_chunks,
-                           ptr(Y), ptr(X), X.shape[1], rank, float(reg), int(bool(implicit)),
+                           ptr(Y), Y.shape[0], ptr(X), X.shape[1], rank, float(reg),
+                           int(bool(implicit)),
                            float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(), int(phases),
                            stream_ptr(X.device)), "als_solve_half")
 

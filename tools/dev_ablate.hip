@@ -31,7 +31,16 @@ __global__ __launch_bounds__(64, 2) void ablate_kernel(const int64_t* __restrict
   const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
   bool gram = MODE == 0 || MODE == 1 || (MODE == 5 && (blockIdx.x & 1));
   if (gram) {
-    gram_accumulate<CN, false, false, float>(col, val, pb, pe, Y, ld, 64, 0.f, tot, bt, npos);
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gram_accumulate_split<CN, false>(col, val, pb, pe, Y, ld, 64, 0.f, 1.f, acc, bt, npos,
+                                     reinterpret_cast<int*>(smem));
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r];
+    __syncthreads();
   } else {
     // synthetic SPD system: small off-diagonals, diagonal from regularisation
 #pragma unroll

@@ -59,12 +59,22 @@ def gram_flops(nnz: int, n_solved: int, k: int) -> float:
     return nnz * (k * (k + 1) + 2 * k) + n_solved * (k ** 3 / 3 + 2 * k ** 2)
 
 
-def load_pmc(kernel_prefix: str):
+def gather_bytes(nnz: int, n_rows: int, k: int) -> float:
+    """Algorithmic bytes of launch 1 of a half-sweep: per rating the gathered fp32
+    factor row (4k) + column index + rating (8 B); per solved row its output row (4k)
+    and row pointer (8 B).  Every byte counted once, no cache reuse assumed."""
+    return nnz * (4 * k + 8) + n_rows * (4 * k + 8)
+
+
+def load_pmc(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (tools/profile.sh -> tools/pmc_summary.py), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(kernel_prefix, {}).get("hbm_bytes_per_launch")
+        ent = d.get(kernel.replace(" ", ""))
+        return None if ent is None else ent.get("hbm_bytes_per_launch")
     except Exception:
         return None
 
@@ -164,7 +174,11 @@ def run_single(args):
     user_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
     f_item = gram_flops(ib.nnz, ib.n_light, k)
     f_user = gram_flops(ub.nnz, ub.n_light, k)
-    achieved = (f_item + f_user) / ((item_ms + user_ms) * 1e-3) / 1e12
+    b_item = gather_bytes(ib.nnz, ib.n_light, k)
+    b_user = gather_bytes(ub.nnz, ub.n_light, k)
+    launch_s = (item_ms + user_ms) * 1e-3
+    achieved = (b_item + b_user) / launch_s / 1e9
+    tflops = (f_item + f_user) / launch_s / 1e12
     avg_launch_us = 1000.0 * (item_ms + user_ms) / 2
     dominant = dominant_kernel(k, imp)
     traffic = load_pmc(dominant)
@@ -198,12 +212,17 @@ def run_single(args):
                    "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz,
                    "rank": k, "regParam": args.reg, "implicitPrefs": imp, "alpha": alpha,
                    "parallelism": "dp1"},
-        "roofline": {"bound": "mfma", "kernel": dominant,
-                     "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+        "roofline": {"bound": "hbm", "kernel": dominant,
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "avg_launch_us": avg_launch_us,
-                     "algorithmic_flops_per_launch": (f_item + f_user) / 2,
-                     "launch_ms": {"item": item_ms, "user": user_ms}},
+                     "algorithmic_bytes_per_launch": (b_item + b_user) / 2,
+                     "launch_ms": {"item": item_ms, "user": user_ms},
+                     "flops_view": {"algorithmic_flops_per_launch": (f_item + f_user) / 2,
+                                    "achieved_tflops": tflops,
+                                    "note": "fp32-grade Gram on f16 MFMA (3 products per "
+                                            "fp32 product, k<=64); peak f16 dense 2500 TF, "
+                                            "fp32 157.3 TF"}},
         "topk10_recs_per_s": core.n_users / (topk_ms * 1e-3),
         "topk10_ms": topk_ms,
         "csr_build_ms": build_ms,

@@ -108,6 +108,12 @@ struct FullTiles {
       for (int c = 0; c < NC; ++c) y[c] = 0.f;
     }
   }
+  // Unconditional load of this lane's dims from row `row` (offsets clamped into
+  // [0, ld): lanes whose dims are >= k read real dims, masked out after the Gram).
+  __device__ static __forceinline__ void load_clamped(const float* __restrict__ row,
+                                                      float (&y)[NC], int d0, int ld) {
+    load_dims<CN>(row + (d0 + CN <= ld ? d0 : ld - CN), y);
+  }
 };
 
 // WgTiles<R>: wavefront R of the 4-wave workgroup that owns one k <= 128 system
@@ -147,6 +153,19 @@ struct WgTiles {
         const float4 v = *reinterpret_cast<const float4*>(p + 4);
         y[2] = v.x; y[3] = v.y; y[4] = v.z; y[5] = v.w;
       }
+    }
+  }
+  __device__ static __forceinline__ void load_clamped(const float* __restrict__ row,
+                                                      float (&y)[NC], int d0, int ld) {
+    auto cl = [&](int o, int w) { return o + w <= ld ? o : ld - w; };
+    if constexpr (R < 2) {
+      const float4 v = *reinterpret_cast<const float4*>(row + cl(d0 + 4 * R, 4));
+      y[0] = v.x; y[1] = v.y; y[2] = v.z; y[3] = v.w;
+    } else {
+      const float2 u = *reinterpret_cast<const float2*>(row + cl(d0 + 2 * (R - 2), 2));
+      const float4 v = *reinterpret_cast<const float4*>(row + cl(d0 + 4, 4));
+      y[0] = u.x; y[1] = u.y;
+      y[2] = v.x; y[3] = v.y; y[4] = v.z; y[5] = v.w;
     }
   }
 };
@@ -319,6 +338,7 @@ template <int NC>
 struct SplitStep {
   float y[8][NC];
   float r[8];
+  unsigned valid;  // bit j: rating j of this lane's slot exists (else weights 0)
 };
 
 // Stage the (column, rating) pairs of one 64-rating block in LDS (wave-private).
@@ -343,43 +363,48 @@ __device__ __forceinline__ void split_issue(SplitStep<TS::NC>& s, const int* __r
   const int ids[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
   s.r[0] = r0.x; s.r[1] = r0.y; s.r[2] = r0.z; s.r[3] = r0.w;
   s.r[4] = r1.x; s.r[5] = r1.y; s.r[6] = r1.z; s.r[7] = r1.w;
+  s.valid = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    if (ids[j] >= 0) {
-      TS::load(Y + (int64_t)ids[j] * ld + d0, s.y[j], d0, k);
-    } else {
-#pragma unroll
-      for (int c = 0; c < TS::NC; ++c) s.y[j][c] = 0.f;
-    }
+    s.valid |= (ids[j] >= 0 ? 1u : 0u) << j;
+    TS::load_clamped(Y + (int64_t)(ids[j] >= 0 ? ids[j] : 0) * ld, s.y[j], d0, ld);
   }
 }
 
-// Consume one step: rhs FMAs, split, 3 f16 MFMAs per tile.
+// Consume one step, part 1 (VALU): rhs FMAs and the hi/lo split of w*y.
 template <class TS, bool IMPLICIT>
-__device__ __forceinline__ void split_consume(const SplitStep<TS::NC>& s, float sc, float alpha,
-                                              floatx4 (&acc)[TS::N], float (&bf)[TS::NRA]) {
+__device__ __forceinline__ void split_prepare(const SplitStep<TS::NC>& s, float sc, float alpha,
+                                              uint32_t (&hi)[TS::NC][4], uint32_t (&lo)[TS::NC][4],
+                                              float (&bf)[TS::NRA]) {
   float w[8], cb[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
+    const bool v = (s.valid >> j) & 1u;
     if constexpr (IMPLICIT) {
       const float c1 = alpha * fabsf(s.r[j]);
-      w[j] = sc * __builtin_sqrtf(c1);
-      cb[j] = s.r[j] > 0.f ? 1.f + c1 : 0.f;
+      w[j] = v ? sc * __builtin_sqrtf(c1) : 0.f;
+      cb[j] = (v && s.r[j] > 0.f) ? 1.f + c1 : 0.f;
     } else {
-      w[j] = sc;
-      cb[j] = s.r[j];
+      w[j] = v ? sc : 0.f;
+      cb[j] = v ? s.r[j] : 0.f;
     }
   }
 #pragma unroll
   for (int c = 0; c < TS::NR; ++c)
 #pragma unroll
     for (int j = 0; j < 8; ++j) bf[c] = fmaf(cb[j], s.y[j][c], bf[c]);
-  uint32_t hi[TS::NC][4], lo[TS::NC][4];
 #pragma unroll
   for (int c = 0; c < TS::NC; ++c)
 #pragma unroll
     for (int p = 0; p < 4; ++p)
       split_pair(w[2 * p] * s.y[2 * p][c], w[2 * p + 1] * s.y[2 * p + 1][c], hi[c][p], lo[c][p]);
+}
+
+// Part 2 (matrix cores): 3 f16 MFMAs per tile.
+template <class TS>
+__device__ __forceinline__ void split_mfma(const uint32_t (&hi)[TS::NC][4],
+                                           const uint32_t (&lo)[TS::NC][4],
+                                           floatx4 (&acc)[TS::N]) {
   static_for<TS::N>([&](auto ti) {
     constexpr int tt = decltype(ti)::value;
     constexpr int a = TS::l1(tt), b = TS::l2(tt);
@@ -418,45 +443,47 @@ __device__ __forceinline__ void gram_accumulate_split(
   const int nsteps = (int)((n + 31) >> 5);
   int ci_n, ci_c;
   float rv_n, rv_c;
+  (void)rv_c;
   load_idx(pb, ci_c, rv_c);
   load_idx(pb + 64, ci_n, rv_n);
   stage_block(st_c, st_r, ci_c, rv_c);
   if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_c >= 0 && rv_c > 0.f));
   wave_lds_sync();
-  SplitStep<TS::NC> sA, sB;
+  // One register set for the gathered rows: step s is split into its f16
+  // operands, then the gathers of step s+1 are issued into the same registers,
+  // then step s's MFMAs run while those loads are in flight.
+  SplitStep<TS::NC> sA;
   split_issue<CN, TS>(sA, st_c, st_r, 0, Y, ld, d0, k);
-  // step s uses block s>>1, half s&1; before issuing step s+1 = 2b+2 the block
-  // b+1 is staged (its pairs were prefetched into ci_n/rv_n one block earlier).
-  auto next = [&](SplitStep<TS::NC>& dst, int s1) {
-    if ((s1 & 1) == 0) {
-      stage_block(st_c, st_r, ci_n, rv_n);
-      if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_n >= 0 && rv_n > 0.f));
-      wave_lds_sync();
-      load_idx(pb + 64 * (int64_t)((s1 >> 1) + 1), ci_n, rv_n);
-    }
-    split_issue<CN, TS>(dst, st_c, st_r, s1 & 1, Y, ld, d0, k);
-  };
-  // rhs: 16-term fp32 partials per lane and 64-rating block, summed into bf
+  // rhs: fp32 partials per lane over 64-rating blocks, summed into bf
   float bp[TS::NRA];
-  auto flush = [&]() {
-#pragma unroll
-    for (int c = 0; c < TS::NRA; ++c) {
-      bf[c] += bp[c];
-      bp[c] = 0.f;
-    }
-  };
 #pragma unroll
   for (int c = 0; c < TS::NRA; ++c) bp[c] = 0.f;
-  int s = 0;
-  for (; s + 2 <= nsteps; s += 2) {
-    next(sB, s + 1);
-    split_consume<TS, IMPLICIT>(sA, sc, alpha, acc, bp);
-    if (s + 2 < nsteps) next(sA, s + 2);
-    split_consume<TS, IMPLICIT>(sB, sc, alpha, acc, bp);
-    flush();
+  for (int s = 0; s < nsteps; ++s) {
+    uint32_t hi[TS::NC][4], lo[TS::NC][4];
+    split_prepare<TS, IMPLICIT>(sA, sc, alpha, hi, lo, bp);
+    const int s1 = s + 1;
+    if (s1 < nsteps) {
+      // step s1 uses block s1>>1, half s1&1; a new block is staged from the
+      // pairs prefetched one block earlier
+      if ((s1 & 1) == 0) {
+        stage_block(st_c, st_r, ci_n, rv_n);
+        if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_n >= 0 && rv_n > 0.f));
+        wave_lds_sync();
+        load_idx(pb + 64 * (int64_t)((s1 >> 1) + 1), ci_n, rv_n);
+      }
+      split_issue<CN, TS>(sA, st_c, st_r, s1 & 1, Y, ld, d0, k);
+    }
+    split_mfma<TS>(hi, lo, acc);
+    if (s & 1) {
+#pragma unroll
+      for (int c = 0; c < TS::NRA; ++c) {
+        bf[c] += bp[c];
+        bp[c] = 0.f;
+      }
+    }
   }
-  if (s < nsteps) split_consume<TS, IMPLICIT>(sA, sc, alpha, acc, bp);
-  flush();
+#pragma unroll
+  for (int c = 0; c < TS::NRA; ++c) bf[c] += bp[c];
 }
 
 // (i, j) of register r of upper tile tt for this lane (MFMA 16x16 C layout:
@@ -518,12 +545,21 @@ __device__ __forceinline__ double readlane_t(double v, int l) { return readlane_
 // B_IJ -= U_KI^T D_K U_KJ (K < I <= J) run on the matrix cores from the U
 // columns in LDS.  Back substitution x_K = U_KK^-1 (z_K / D_K - sum_J U_KJ x_J)
 // on 16 lanes (DPP row broadcasts).
-// LDS (floats): tile slots NT x 320 (16 columns, stride 20: conflict-free MFMA
-// operand reads) | z, d, x 3 x 16 NB.
+// LDS (floats): tile slots NT x 288 (16 columns, stride 18: 8-B aligned, at
+// most 2-way conflicts on the MFMA operand reads) | z, d, x 3 x 16 NB.
 // ---------------------------------------------------------------------------
+// This lane's id, opaque to the optimizer: per-pivot lane masks are then
+// computed where they are used instead of being hoisted into (and spilling)
+// scalar registers across the unrolled pivot loops.
+__device__ __forceinline__ int lane_opaque() {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
 template <int CN>
 struct PanelLds {
-  static constexpr int NB = CN, NT = CN * (CN + 1) / 2, CS = 20;  // column stride
+  static constexpr int NB = CN, NT = CN * (CN + 1) / 2, CS = 18;  // column stride
   static constexpr int T = 0, Z = NT * 16 * CS, D = Z + 16 * NB, X = D + 16 * NB,
                        SIZE = X + 16 * NB;
 };
@@ -560,6 +596,43 @@ __device__ __forceinline__ float newbcast(float v) {  // lane P of each 16-lane 
                                                                 0x150 + P, 0xF, 0xF, false));
 }
 
+// Block back substitution x_K = U_KK^-1 (z_K / D_K - sum_{J>K} U_KJ x_J) on lanes
+// 0..15 (lanes 16.. mirror), K = NB-1 .. 0, from the U columns in the tile slots
+// (column-major, stride CS; the U_KK columns hold 0 on and below the diagonal, so
+// no masks are needed).  Runtime block loops keep the LDS address arithmetic
+// out of the registers of the unrolled solve.
+template <int CS>
+__device__ __forceinline__ void block_back_subst(int NB, const float* __restrict__ tiles,
+                                                 const float* __restrict__ Zv,
+                                                 const float* __restrict__ Dv,
+                                                 float* __restrict__ Xv) {
+  const int lane = threadIdx.x & 63, i = lane & 15;
+  for (int K = NB - 1; K >= 0; --K) {
+    float v = Zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
+    for (int J = K + 1; J < NB; ++J) {
+      const float* U = tiles + tile_index(NB, K, J) * 16 * CS + i;
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const float4 xj = *reinterpret_cast<const float4*>(Xv + J * 16 + 4 * j4);
+        v = fmaf(-U[(4 * j4 + 0) * CS], xj.x, v);
+        v = fmaf(-U[(4 * j4 + 1) * CS], xj.y, v);
+        v = fmaf(-U[(4 * j4 + 2) * CS], xj.z, v);
+        v = fmaf(-U[(4 * j4 + 3) * CS], xj.w, v);
+      }
+    }
+    const float* Ukk = tiles + tile_index(NB, K, K) * 16 * CS + i;
+    float u[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) u[j] = Ukk[j * CS];
+    static_for<16>([&](auto jr) {
+      constexpr int j = 15 - decltype(jr)::value;
+      v = fmaf(-u[j], newbcast<j>(v), v);
+    });
+    if (lane < 16) Xv[K * 16 + i] = v;
+    wave_lds_sync();
+  }
+}
+
 template <int CN>
 __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const float (&bq)[CN],
                                                 float* __restrict__ lds, int k,
@@ -584,7 +657,9 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     static_for<NB - K>([&](auto jc) {
       constexpr int J = K + decltype(jc)::value;
       const floatx4 v = A[tile_index(NB, K, J)];
-      *reinterpret_cast<float4*>(slot(K, J) + m * CS + 4 * q) = make_float4(v[0], v[1], v[2], v[3]);
+      float2* dst = reinterpret_cast<float2*>(slot(K, J) + m * CS + 4 * q);
+      dst[0] = make_float2(v[0], v[1]);
+      dst[1] = make_float2(v[2], v[3]);
     });
     wave_lds_sync();
     const bool col_ok = lane < NCOL;
@@ -592,9 +667,9 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     float* colp = slot(K, Jl) + m * CS;
     float R[16];
 #pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) {
-      const float4 v = *reinterpret_cast<const float4*>(colp + 4 * c4);
-      R[4 * c4] = v.x; R[4 * c4 + 1] = v.y; R[4 * c4 + 2] = v.z; R[4 * c4 + 3] = v.w;
+    for (int c2 = 0; c2 < 8; ++c2) {
+      const float2 v = *reinterpret_cast<const float2*>(colp + 2 * c2);
+      R[2 * c2] = v.x; R[2 * c2 + 1] = v.y;
     }
     // (b) 16 pivots over the whole panel (diag LDL^T + TRSM + rhs forward)
     float myd = 1.f;
@@ -604,19 +679,19 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
       ok = ok && (d > 0.f);
       const float rd = rcp_t(d);
       const float bp = readlane_t(rb, p);
-      const float f = lane > p ? R[p] * rd : 0.f;  // U[p][t]; 0 below the diagonal
+      const int lo = lane_opaque();
+      const float f = lo > p ? R[p] * rd : 0.f;  // U[p][t]; 0 below the diagonal
       rb = fmaf(-f, bp, rb);
 #pragma unroll
       for (int i = p + 1; i < 16; ++i) R[i] = fmaf(-readlane_t(R[i], p), f, R[i]);
       R[p] = f;
-      if (lane == p) myd = d;
+      if (lo == p) myd = d;
     }
     // (c) U columns -> tile slots (block row K); z_K, D_K
     if (col_ok) {
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4)
-        *reinterpret_cast<float4*>(colp + 4 * c4) =
-            make_float4(R[4 * c4], R[4 * c4 + 1], R[4 * c4 + 2], R[4 * c4 + 3]);
+      for (int c2 = 0; c2 < 8; ++c2)
+        *reinterpret_cast<float2*>(colp + 2 * c2) = make_float2(R[2 * c2], R[2 * c2 + 1]);
     }
     if (lane < 16) {
       Zv[K * 16 + lane] = rb;
@@ -647,35 +722,8 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     }
   });
   wave_lds_sync();
-  // (e) back substitution on lanes 0..15 (lanes 16.. mirror): U_KK columns hold 0
-  // on and below the diagonal, so no masks are needed.
-  const int i = m;
-  static_for<NB>([&](auto kr) {
-    constexpr int K = NB - 1 - decltype(kr)::value;
-    float v = Zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
-    static_for<NB - 1 - K>([&](auto jc) {
-      constexpr int J = K + 1 + decltype(jc)::value;
-      const float* U = slot(K, J);
-#pragma unroll
-      for (int j4 = 0; j4 < 4; ++j4) {
-        const float4 xj = *reinterpret_cast<const float4*>(Xv + J * 16 + 4 * j4);
-        v = fmaf(-U[(4 * j4 + 0) * CS + i], xj.x, v);
-        v = fmaf(-U[(4 * j4 + 1) * CS + i], xj.y, v);
-        v = fmaf(-U[(4 * j4 + 2) * CS + i], xj.z, v);
-        v = fmaf(-U[(4 * j4 + 3) * CS + i], xj.w, v);
-      }
-    });
-    const float* Ukk = slot(K, K);
-    float u[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) u[j] = Ukk[j * CS + i];
-    static_for<16>([&](auto jr) {
-      constexpr int j = 15 - decltype(jr)::value;
-      v = fmaf(-u[j], newbcast<j>(v), v);
-    });
-    if (lane < 16) Xv[K * 16 + i] = v;
-    wave_lds_sync();
-  });
+  // (e) back substitution
+  block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);
   // (f) un-permute: dim d = i*CN + K  <->  Xv[K*16 + i]
   for (int d = lane; d < ld; d += 64) {
     const float x = d < 16 * CN ? Xv[(d % CN) * 16 + d / CN] : 0.f;
@@ -706,12 +754,13 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
                                                  int32_t* __restrict__ status) {
   constexpr int NT = Cfg<CN>::NT;
   float bq[CN];
+  const int m = threadIdx.x & 15;
 #pragma unroll
   for (int c = 0; c < CN; ++c) {
     AccT v = bt[c];
     v += shfl_xor_t(v, 16);
     v += shfl_xor_t(v, 32);
-    bq[c] = (float)v;
+    bq[c] = m * CN + c < k ? (float)v : 0.f;  // padded dims: rhs 0
   }
   floatx4 A[NT];
   int tt = 0;
@@ -729,6 +778,9 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
         } else {
           A[tt][r] = (float)tot[tt][r];
         }
+        int i, j;
+        tile_ij<CN>(c1, c2, r, i, j);
+        if (i >= k || j >= k) A[tt][r] = 0.f;  // padded dims: rows/columns of the identity
       }
       ++tt;
     }
@@ -787,7 +839,7 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 // task (<= chunk ratings), fp64 across the chunks of a heavy row.
 // scal[0] = max |Y| (als_absmax_kernel), scal[1] = max |rating| (implicit).
 template <int CN, bool IMPLICIT>
-__global__ __launch_bounds__(64, 2) void gram_solve_kernel(
+__global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ light_rows,
     const int32_t* __restrict__ chunk_row, const int64_t* __restrict__ chunk_begin,
@@ -923,135 +975,100 @@ __global__ __launch_bounds__(64) void yty_reduce_kernel(const double* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// k in (64, 128]: one workgroup of 4 wavefronts per system (CN = 8, 36 upper
-// tiles).  Wave R accumulates the tiles of WgTiles<R> (10/10/8/8) and keeps them
-// in registers through the factorisation; the block LDL^T of tile_ldl_solve is
-// spread over the workgroup:
-//   (a) owners stage block row K (transposed) in LDS            | barrier
-//   (b) wave 0: 16x16 LDL^T of B_KK with the rhs block z_K      | barrier
-//   (c) TRSM, lane g = 64 R + lane owns column g of block row K  | barrier
-//   (d) each wave: MFMA trailing update of its own tiles (I > K)
-// and wave 0 runs the block back substitution.  (c) writes W into its own
-// buffer, so the stage may be rewritten by the next K without another barrier.
-// LDS (floats): U tiles 36*256 | stage 8*320 | W 7*256 | D, b, z, x 4*128 = 56 KB,
-// so two workgroups (8 waves, 2 per SIMD) share a CU.
+// k in (64, 128]: one workgroup of 4 wavefronts per system (CN = 8, NB = 8
+// block rows, 36 upper tiles).  Wave R accumulates the tiles of WgTiles<R>
+// (10/10/8/8) with the split f16 Gram and keeps them in registers through the
+// factorisation.  The panel LDL^T of panel_ldl_solve, spread over the waves:
+//   (a) owners write block row K (column-major) to the tile slots  | barrier
+//   (b) wave w: lanes 0..15 the diagonal block (every wave, the same
+//       arithmetic; wave 0 publishes it), lanes 16..63 the off-diagonal tiles
+//       J = K+1+3w .. K+3+3w; U columns and updated rhs back to LDS  | barrier
+//   (c) each wave: MFMA trailing update of its own tiles (I > K)
+// then wave 0 back-substitutes.  The rhs of column j of tile J lives in RB[16J+j]
+// between block rows.
+// LDS (floats): tile slots 36 x 288 | z, d, x, rb 4 x 128 = 43.5 KB: three
+// workgroups (12 waves, 3 per SIMD) per CU.
 // ---------------------------------------------------------------------------
 constexpr int kWgNB = 8;
 
 struct WgLds {
-  static constexpr int NB = kWgNB, NT = NB * (NB + 1) / 2;
-  static constexpr int U = 0, S = NT * 256, W = S + NB * 320, D = W + (NB - 1) * 256,
-                       B = D + 16 * NB, Z = B + 16 * NB, X = Z + 16 * NB, SIZE = X + 16 * NB;
+  static constexpr int NB = kWgNB, NT = NB * (NB + 1) / 2, CS = 18;
+  static constexpr int T = 0, Z = NT * 16 * CS, D = Z + 16 * NB, X = D + 16 * NB,
+                       RB = X + 16 * NB, SIZE = RB + 16 * NB;
 };
 
-
 template <int R>
-__device__ __forceinline__ bool wg_ldl_solve(floatx4 (&A)[WgTiles<R>::N], float* __restrict__ lds,
-                                             int k, float* __restrict__ xrow, int ld) {
+__device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], float* __restrict__ lds,
+                                               int k, float* __restrict__ xrow, int ld) {
   typedef WgTiles<R> TS;
   typedef WgLds Lo;
-  constexpr int NB = kWgNB;
+  constexpr int NB = kWgNB, CS = Lo::CS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  const int i = lane & 15;
-  float* Ust = lds + Lo::U;
-  float* St = lds + Lo::S;
-  float* Wb = lds + Lo::W;
+  float* Zv = lds + Lo::Z;
   float* Dv = lds + Lo::D;
-  float* bv = lds + Lo::B;
-  float* zv = lds + Lo::Z;
-  float* xv = lds + Lo::X;
+  float* Xv = lds + Lo::X;
+  float* RBv = lds + Lo::RB;
+  auto slot = [&](int I, int J) { return lds + Lo::T + tile_index(NB, I, J) * 16 * CS; };
   bool ok = true;
   static_for<NB>([&](auto Kc) {
     constexpr int K = decltype(Kc)::value;
-    // (a) stage block row K transposed: St[J-K][j][k] (row stride 20 floats)
+    // (a) owners: block row K -> column-major slots
     static_for<TS::N>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
       if constexpr (TS::g1(t) == K) {
-        constexpr int J = TS::g2(t);
         const floatx4 v = A[t];
-        *reinterpret_cast<float4*>(St + (J - K) * 320 + m * 20 + 4 * q) =
-            make_float4(v[0], v[1], v[2], v[3]);
+        float2* dst = reinterpret_cast<float2*>(slot(K, TS::g2(t)) + m * CS + 4 * q);
+        dst[0] = make_float2(v[0], v[1]);
+        dst[1] = make_float2(v[2], v[3]);
       }
     });
     __syncthreads();
-    // (b) LDL^T of the diagonal block, rhs block as augmented column (wave 0)
-    if constexpr (R == 0) {
-      float a[16];
+    // (b) panel: lanes 0..15 diagonal block, lanes 16.. tiles K+1+3R ..
+    constexpr int NOFF = NB - 1 - K;  // off-diagonal tiles in block row K
+    if constexpr (R == 0 || 3 * R < NOFF) {
+      const int Jl0 = q == 0 ? K : K + 3 * R + q;
+      const bool col_ok = Jl0 < NB;
+      const int Jl = col_ok ? Jl0 : K;
+      float* colp = slot(K, Jl) + m * CS;
+      float R16[16];
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const float4 v = *reinterpret_cast<const float4*>(St + i * 20 + 4 * c4);
-        a[4 * c4] = v.x; a[4 * c4 + 1] = v.y; a[4 * c4 + 2] = v.z; a[4 * c4 + 3] = v.w;
+      for (int c2 = 0; c2 < 8; ++c2) {
+        const float2 v = *reinterpret_cast<const float2*>(colp + 2 * c2);
+        R16[2 * c2] = v.x; R16[2 * c2 + 1] = v.y;
       }
-      float bb = bv[K * 16 + i];
+      float rb = RBv[16 * Jl + m];
       float myd = 1.f;
 #pragma unroll
       for (int p = 0; p < 16; ++p) {
-        const float d = readlane_t(a[p], p);
+        const float d = readlane_t(R16[p], p);
         ok = ok && (d > 0.f);
-        float u[16];
+        const float rd = rcp_t(d);
+        const float bp = readlane_t(rb, p);
+        const int lo = lane_opaque();
+        const float f = lo > p ? R16[p] * rd : 0.f;
+        rb = fmaf(-f, bp, rb);
 #pragma unroll
-        for (int j = p + 1; j < 16; ++j) u[j] = readlane_t(a[p], j);
-        const float bp = readlane_t(bb, p);
-        const float l = a[p] * rcp_t(d);
-#pragma unroll
-        for (int j = p + 1; j < 16; ++j) a[j] = fmaf(-l, u[j], a[j]);
-        if (i > p) bb = fmaf(-l, bp, bb);
-        a[p] = l;
-        if (i == p) myd = d;
+        for (int i = p + 1; i < 16; ++i) R16[i] = fmaf(-readlane_t(R16[i], p), f, R16[i]);
+        R16[p] = f;
+        if (lo == p) myd = d;
       }
-      float* Lt = Ust + 256 * tile_index(NB, K, K);  // Lt[c*16 + r] = L_K[r][c]
-      if (lane < 16) {
-        Dv[K * 16 + i] = myd;
-        zv[K * 16 + i] = bb;
+      if (col_ok && (q > 0 || R == 0)) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c) Lt[c * 16 + i] = (c < i) ? a[c] : 0.f;
+        for (int c2 = 0; c2 < 8; ++c2)
+          *reinterpret_cast<float2*>(colp + 2 * c2) = make_float2(R16[2 * c2], R16[2 * c2 + 1]);
+        RBv[16 * Jl + m] = rb;
+      }
+      if (R == 0 && lane < 16) {
+        Zv[K * 16 + lane] = rb;
+        Dv[K * 16 + lane] = myd;
       }
     }
     __syncthreads();
+    // (c) trailing update of this wave's tiles: B_IJ -= (D_K U_KI)^T U_KJ
     if constexpr (K + 1 < NB) {
-      constexpr int ncol = 16 * (NB - 1 - K);
-      // (c) TRSM: g = 64 R + lane < ncol owns column (g & 15) of block J = K+1+(g>>4)
-      if constexpr (64 * R < ncol) {
-        const int g = 64 * R + lane;
-        const bool is_col = g < ncol;
-        const int Jl = K + 1 + (is_col ? (g >> 4) : 0);
-        const float* Lt = Ust + 256 * tile_index(NB, K, K);
-        float w[16];
-        {
-          const float* src = St + (Jl - K) * 320 + i * 20;
+      float dq[4];
 #pragma unroll
-          for (int c4 = 0; c4 < 4; ++c4) {
-            const float4 v = *reinterpret_cast<const float4*>(src + 4 * c4);
-            w[4 * c4] = v.x; w[4 * c4 + 1] = v.y; w[4 * c4 + 2] = v.z; w[4 * c4 + 3] = v.w;
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 15; ++c) {
-          float lc[16];
-#pragma unroll
-          for (int c4 = 0; c4 < 4; ++c4) {
-            const float4 v = *reinterpret_cast<const float4*>(Lt + c * 16 + 4 * c4);
-            lc[4 * c4] = v.x; lc[4 * c4 + 1] = v.y; lc[4 * c4 + 2] = v.z; lc[4 * c4 + 3] = v.w;
-          }
-#pragma unroll
-          for (int p = c + 1; p < 16; ++p) w[p] = fmaf(-lc[p], w[c], w[p]);
-        }
-        if (is_col) {
-          float* Wd = Wb + (Jl - K - 1) * 256 + i;
-          float* Ud = Ust + 256 * tile_index(NB, K, Jl) + i;
-          float t = 0.f;
-#pragma unroll
-          for (int c = 0; c < 16; ++c) {
-            const float uc = w[c] * rcp_t(Dv[K * 16 + c]);
-            Wd[c * 16] = w[c];
-            Ud[c * 16] = uc;
-            t = fmaf(uc, zv[K * 16 + c], t);
-          }
-          bv[Jl * 16 + i] -= t;  // b_J -= U_KJ^T z_K
-        }
-      }
-      __syncthreads();
-      // (d) trailing update of this wave's tiles on the matrix cores
+      for (int s4 = 0; s4 < 4; ++s4) dq[s4] = -Dv[K * 16 + 4 * s4 + q];
       static_for<TS::N>([&](auto tc) {
         constexpr int t = decltype(tc)::value;
         constexpr int I = TS::g1(t), J = TS::g2(t);
@@ -1059,42 +1076,21 @@ __device__ __forceinline__ bool wg_ldl_solve(floatx4 (&A)[WgTiles<R>::N], float*
           floatx4 acc = A[t];
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                -Ust[256 * tile_index(NB, K, I) + (4 * s4 + q) * 16 + m],
-                Wb[(J - K - 1) * 256 + (4 * s4 + q) * 16 + m], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dq[s4] * slot(K, I)[m * CS + 4 * s4 + q],
+                                                        slot(K, J)[m * CS + 4 * s4 + q], acc, 0,
+                                                        0, 0);
           A[t] = acc;
+          asm volatile("" ::: "memory");
         }
       });
     }
   });
   if constexpr (R == 0) {
-    // (e) block back substitution (wave 0): x_K = U_KK^-1 (D_K^-1 z_K - sum_J U_KJ x_J)
-#pragma unroll
-    for (int K = NB - 1; K >= 0; --K) {
-      float v = zv[K * 16 + i] * rcp_t(Dv[K * 16 + i]);
-#pragma unroll
-      for (int J = K + 1; J < NB; ++J) {
-        const float* Ur = Ust + 256 * tile_index(NB, K, J) + i * 16;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v = fmaf(-Ur[j], xv[J * 16 + j], v);
-      }
-      const float* Lr = Ust + 256 * tile_index(NB, K, K) + i * 16;
-      float ur[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) ur[j] = Lr[j];
-      float x = 0.f;
-#pragma unroll
-      for (int j = 15; j >= 0; --j) {
-        const float xj = readlane_t(v, j);
-        if (i == j) x = xj;
-        if (i < j) v = fmaf(-ur[j], xj, v);
-      }
-      if (lane < 16) xv[K * 16 + i] = x;
-      wave_lds_sync();
-    }
-    // (f) un-permute: dim d = i*8 + K  <->  xv[K*16 + i]
+    // (d) back substitution
+    block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);
+    // (e) un-permute: dim d = i*8 + K  <->  Xv[K*16 + i]
     for (int d = lane; d < ld; d += 64) {
-      const float x = d < 16 * NB ? xv[(d % NB) * 16 + d / NB] : 0.f;
+      const float x = d < 16 * NB ? Xv[(d % NB) * 16 + d / NB] : 0.f;
       xrow[d] = (d < k && ok) ? x : 0.f;
     }
   }
@@ -1102,7 +1098,7 @@ __device__ __forceinline__ bool wg_ldl_solve(floatx4 (&A)[WgTiles<R>::N], float*
 }
 
 // Wave R's part of completing one system: rhs blocks to LDS, YtY merge (fp64,
-// then one rounding), lambda * n on the diagonal, the workgroup LDL^T.
+// then one rounding), lambda * n on the diagonal, the workgroup panel LDL^T.
 template <int R, bool IMPLICIT, class AccT>
 __device__ __forceinline__ void wg_finish_and_solve(AccT (&tot)[WgTiles<R>::N][4],
                                                     AccT (&bt)[WgTiles<R>::NRA], int64_t n_reg,
@@ -1118,7 +1114,7 @@ __device__ __forceinline__ void wg_finish_and_solve(AccT (&tot)[WgTiles<R>::N][4
     AccT v = bt[c];
     v += shfl_xor_t(v, 16);
     v += shfl_xor_t(v, 32);
-    if (q == 0) lds[WgLds::B + TS::gcol(c) * 16 + m] = (float)v;
+    if (q == 0) lds[WgLds::RB + TS::gcol(c) * 16 + m] = m * NB + TS::gcol(c) < k ? (float)v : 0.f;
   }
   const float lam = (float)((double)reg * (double)n_reg);
   floatx4 A[TS::N];
@@ -1136,11 +1132,12 @@ __device__ __forceinline__ void wg_finish_and_solve(AccT (&tot)[WgTiles<R>::N][4
       } else {
         v = (float)tot[t][r];
       }
+      if (i >= k || j >= k) v = 0.f;  // padded dims: identity rows/columns
       if (c1 == c2 && i == j) v = (i < k) ? v + lam : 1.f;
       A[t][r] = v;
     }
   });
-  const bool ok = wg_ldl_solve<R>(A, lds, k, xrow, ld);
+  const bool ok = wg_panel_solve<R>(A, lds, k, xrow, ld);
   if (R == 0 && !ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -1154,21 +1151,39 @@ __device__ __forceinline__ void wg_gram_solve_task(
     const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
     int32_t n_chunks, const float* __restrict__ Y, float* __restrict__ X, int ld, int k,
     float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
-    int32_t* __restrict__ status, float* lds) {
+    int32_t* __restrict__ status, float* lds, const float* __restrict__ scal) {
   typedef WgTiles<R> TS;
+  const float wmax = IMPLICIT ? __builtin_sqrtf(alpha * scal[1]) : 1.f;
+  const int e = split_exponent(scal[0] * wmax);
+  const float sc = ldexpf(1.f, e), inv2 = ldexpf(1.f, -2 * e);
+  floatx4 acc[TS::N];
+#pragma unroll
+  for (int t = 0; t < TS::N; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
   float tot[TS::N][4], bt[TS::NRA];
-  zero_acc<TS::N, TS::NRA, float>(tot, bt);
+#pragma unroll
+  for (int c = 0; c < TS::NRA; ++c) bt[c] = 0.f;
   int npos = 0;
+  int64_t pb, pe;
+  int row = -1;
   if (task < n_chunks) {
-    gram_accumulate<kWgNB, IMPLICIT, false, float, TS>(col, val, chunk_begin[task], chunk_end[task],
-                                                       Y, ld, k, alpha, tot, bt, npos);
+    pb = chunk_begin[task];
+    pe = chunk_end[task];
+  } else {
+    row = light_rows[task - n_chunks];
+    pb = row_ptr[row];
+    pe = row_ptr[row + 1];
+  }
+  gram_accumulate_split<kWgNB, IMPLICIT, TS>(col, val, pb, pe, Y, ld, k, alpha, sc, acc, bt, npos,
+                                             reinterpret_cast<int*>(lds) + 128 * R);
+#pragma unroll
+  for (int t = 0; t < TS::N; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
+  if (task < n_chunks) {
     store_slot<TS::N, TS::NRA, float>(slots + (int64_t)task * kWgSlot + R * kWgSub, tot, bt, npos);
     return;
   }
-  const int row = light_rows[task - n_chunks];
-  const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
-  gram_accumulate<kWgNB, IMPLICIT, false, float, TS>(col, val, pb, pe, Y, ld, k, alpha, tot, bt,
-                                                     npos);
+  __syncthreads();  // staging area is reused by the solve
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
   wg_finish_and_solve<R, IMPLICIT, float>(tot, bt, n_reg, lds, k, reg, yty, X + (int64_t)row * ld,
                                           ld, row, status);
@@ -1251,18 +1266,18 @@ __global__ __launch_bounds__(256, 2) void gram_solve_wg_kernel(
     const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
     int32_t n_chunks, const float* __restrict__ Y, float* __restrict__ X, int ld, int k,
     float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, const float* __restrict__ scal) {
   __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
 #define CALL(R)                                                                                 \
   wg_gram_solve_task<R, IMPLICIT>(blockIdx.x, row_ptr, col, val, light_rows, chunk_begin,      \
                                   chunk_end, n_chunks, Y, X, ld, k, reg, alpha, yty, slots,   \
-                                  status, lds)
+                                  status, lds, scal)
   ALS_WG_ROLES(CALL);
 #undef CALL
 }
 
 template <bool IMPLICIT>
-__global__ __launch_bounds__(256, 2) void reduce_solve_wg_kernel(
+__global__ __launch_bounds__(256, 3) void reduce_solve_wg_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
     const int32_t* __restrict__ slot_begin, const double* __restrict__ slots,
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
@@ -1348,7 +1363,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const float* scal = reinterpret_cast<const float*>(scal_u);
   const int cn = cn_for_k(k);
   ALS_REQUIRE(phases >= 1 && phases <= 3, ALS_EINVAL, "als_solve_half: phases must be 1, 2 or 3");
-  if ((phases & 1) && n_chunks + n_light > 0 && cn <= 4) {
+  if ((phases & 1) && n_chunks + n_light > 0) {
     ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
     const int64_t ny = n_src * (int64_t)ld;
     if (ny > 0) {
@@ -1384,7 +1399,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     if (g1)                                                                                       \
       gram_solve_wg_kernel<IMP><<<g1, 256, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,   \
                                                     chunk_end, n_chunks, Y_src, X_dst, ld, k,     \
-                                                    reg, alpha, yty_packed, slots, status_dev);   \
+                                                    reg, alpha, yty_packed, slots, status_dev,    \
+                                                    scal);                                        \
     ALS_LAUNCH_CHECK();                                                                           \
     if (g2)                                                                                       \
       reduce_solve_wg_kernel<IMP><<<g2, 256, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \

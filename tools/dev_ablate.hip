@@ -14,7 +14,7 @@ void set_error(const char*, ...) {}
 namespace als {
 
 template <int MODE>
-__global__ __launch_bounds__(64, 2) void ablate_kernel(const int64_t* __restrict__ row_ptr,
+__global__ __launch_bounds__(64, 3) void ablate_kernel(const int64_t* __restrict__ row_ptr,
                                                        const int32_t* __restrict__ col,
                                                        const float* __restrict__ val,
                                                        const int32_t* __restrict__ rows, int n,

@@ -33,12 +33,9 @@ if stats:
 
 
 def short(name):
-    name = name.split("(")[0]
-    for k in ("gram_solve_kernel", "reduce_solve_kernel", "topk_kernel", "yty_partial_kernel",
-              "rs_scatter_kernel", "predict_kernel", "rmse_partial_kernel"):
-        if k in name:
-            return k
-    return name[-60:]
+    """'void als::gram_solve_kernel<4, false>(long const*, ...)' -> 'gram_solve_kernel<4,false>'"""
+    name = name.split("(")[0].replace("void ", "").replace("als::", "").replace(" ", "")
+    return name[-80:]
 
 
 def counters(path, counter):

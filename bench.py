@@ -142,6 +142,7 @@ def run_single(args):
         # Spark order: items from users, then users from items (ALS.train loop);
         # implicit: YtY of the source side before each half-sweep (computeYtY)
         yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
+        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 4)
         if evs is not None:
             evs[0].record()
         E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
@@ -149,6 +150,7 @@ def run_single(args):
             evs[1].record()
         E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 2)
         yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
+        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 4)
         if evs is not None:
             evs[2].record()
         E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)

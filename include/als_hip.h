@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 2
+#define ALS_ABI_VERSION 3
 
 #define ALS_OK 0
 #define ALS_EINVAL (-1)   /* bad argument (shape, null pointer, rank) */
@@ -94,22 +94,26 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  *   explicit:  A_j = sum_s y_s y_s^T + reg*n_j*I,          b_j = sum_s r_js y_s
  *   implicit:  A_j = YtY + sum_s c1 y_s y_s^T + reg*n+_j*I, b_j = sum_{r>0} (1+c1) y_s,
  *              c1 = alpha*|r|, n+_j = #{r_js > 0}
- * from fp32 factors.  k <= 64: the Gram runs on the f16 matrix cores with every
- * value split into two f16 halves (hi*hi + hi*lo + lo*hi, ~2^-21 relative per
- * product, after a power-of-two scaling by max |Y_src| over its n_src rows, and
- * max |rating| for implicit); 64 < k <= 128: exact fp32 products.  fp32 sums within
- * a task of <= 2048 ratings, fp64 across a heavy row's tasks; solved by a
- * square-root-free block LDL^T (the solution of Spark's Cholesky dppsv) in fp32
- * on the matrix cores, stored fp32 into X_dst[row*ld ..].  k <= 128.
- * Measured against an fp64 restatement: <= 3.2e-6 relative per row (parity bar
+ * from fp32 factors.  The Gram runs on the f16 matrix cores with every value
+ * split into two f16 halves (hi*hi + hi*lo + lo*hi: ~2^-21 relative per product)
+ * after a power-of-two scaling set by max |Y_src| over its n_src rows and
+ * max |rating|.  Explicit: Y_src is split once per call into a table in the
+ * workspace ((n_src + 1) x k_pad words) and the rhs runs on the matrix cores too;
+ * implicit: the split follows the per-rating confidence weight, in registers.
+ * fp32 sums within a task of <= 2048 ratings, fp64 across a heavy row's tasks;
+ * solved by a square-root-free block LDL^T (the solution of Spark's Cholesky
+ * dppsv) in fp32, stored fp32 into X_dst[row*ld ..].  k <= 128, n_src < 2^31.
+ * Measured against an fp64 restatement: <= 5e-6 relative per row (parity bar
  * 1e-4, tests/test_gpu_kernels.py).  yty_packed (implicit only): lower-packed
  * fp64 k_pad x k_pad Gram from als_yty.  status_dev: device int32, set to
  * (row+1) of a row whose Cholesky pivot was not positive (0 = all rows ok;
- * Spark raises from dppsv in that case).
- * phases: bit 0 = launch 1 (heavy-row chunk partials + fused light-row
- * gram/solve), bit 1 = launch 2 (heavy-row reduce + solve); 3 = both (the
- * normal call; launch 2 must follow launch 1 on the same stream). */
-size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks);
+ * Spark raises from dppsv in that case).  ws: 16-byte aligned.
+ * phases: bit 2 = prep (scale words; explicit: the split table of Y_src),
+ * bit 0 = launch 1 (heavy-row chunk partials + fused light-row gram/solve),
+ * bit 1 = launch 2 (heavy-row reduce + solve); 7 = all (the normal call).  They
+ * run in the order prep, 1, 2; split across calls, issue them in that order on
+ * one stream with the same workspace. */
+size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src);
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light,
                    const int32_t* heavy_rows, const int32_t* heavy_slot_begin, int32_t n_heavy,

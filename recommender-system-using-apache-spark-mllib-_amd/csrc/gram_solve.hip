@@ -114,6 +114,20 @@ struct FullTiles {
                                                       float (&y)[NC], int d0, int ld) {
     load_dims<CN>(row + (d0 + CN <= ld ? d0 : ld - CN), y);
   }
+  // This lane's NC words of a pre-split row (p = row + m*CN; rows are kp = 16*CN wide).
+  __device__ static __forceinline__ void load_pre(const uint32_t* __restrict__ p,
+                                                  uint32_t (&w)[NC]) {
+    if constexpr (CN == 1) {
+      w[0] = p[0];
+    } else if constexpr (CN == 2) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      w[0] = v.x; w[1] = v.y;
+    } else {
+      static_assert(CN == 4, "pre-split rows: CN in {1, 2, 4}");
+      const uint4 v = *reinterpret_cast<const uint4*>(p);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    }
+  }
 };
 
 // WgTiles<R>: wavefront R of the 4-wave workgroup that owns one k <= 128 system
@@ -166,6 +180,18 @@ struct WgTiles {
       const float4 v = *reinterpret_cast<const float4*>(row + cl(d0 + 4, 4));
       y[0] = u.x; y[1] = u.y;
       y[2] = v.x; y[3] = v.y; y[4] = v.z; y[5] = v.w;
+    }
+  }
+  __device__ static __forceinline__ void load_pre(const uint32_t* __restrict__ p,
+                                                  uint32_t (&w)[NC]) {
+    if constexpr (R < 2) {
+      const uint4 v = *reinterpret_cast<const uint4*>(p + 4 * R);
+      w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+      const uint2 u = *reinterpret_cast<const uint2*>(p + 2 * (R - 2));
+      const uint4 v = *reinterpret_cast<const uint4*>(p + 4);
+      w[0] = u.x; w[1] = u.y;
+      w[2] = v.x; w[3] = v.y; w[4] = v.z; w[5] = v.w;
     }
   }
 };
@@ -484,6 +510,207 @@ __device__ __forceinline__ void gram_accumulate_split(
   }
 #pragma unroll
   for (int c = 0; c < TS::NRA; ++c) bf[c] += bp[c];
+}
+
+// ---------------------------------------------------------------------------
+// Explicit feedback: the Gram is unweighted, so every factor row is split once
+// per half-sweep into a table (split_table_kernel): Ysp[row][d] = f16 hi |
+// f16 lo << 16 of 2^ey * Y[row][d] (padding dims and the extra row n_src zero).
+// The Gram loop then gathers 4 B per dim (as for fp32) and forms its f16
+// operands with v_perm_b32 alone.  Ratings are split the same way (2^er * r)
+// when a 64-rating block is staged, and the rhs b = sum r y runs on the matrix
+// cores too: B operand column 0 = hi(r), column 1 = lo(r), all other columns 0,
+// so C[i][0] + C[i][1] = sum (hi_y + lo_y)(hi_r + lo_r).  Ratings past the end
+// of the row point at the zero row and add nothing.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t split_word(float t) {
+  const _Float16 h = (_Float16)t;  // round to nearest
+  const _Float16 l = (_Float16)(t - (float)h);
+  return (uint32_t)__builtin_bit_cast(unsigned short, h) |
+         ((uint32_t)__builtin_bit_cast(unsigned short, l) << 16);
+}
+
+template <int NC>
+struct PreStep {
+  uint32_t w[8][NC];  // split words: rating j of this lane's slot, its NC dims
+  uint32_t r[8];      // split words of those ratings
+};
+
+template <class TS>
+__device__ __forceinline__ void pre_issue(PreStep<TS::NC>& s, const int* __restrict__ st_c,
+                                          const uint32_t* __restrict__ st_r, int h,
+                                          const uint32_t* __restrict__ base, uint32_t kp) {
+  const int q = (threadIdx.x & 63) >> 4;
+  const int o = 32 * h + 8 * q;
+  const int4 c0 = *reinterpret_cast<const int4*>(st_c + o);
+  const int4 c1 = *reinterpret_cast<const int4*>(st_c + o + 4);
+  const uint4 r0 = *reinterpret_cast<const uint4*>(st_r + o);
+  const uint4 r1 = *reinterpret_cast<const uint4*>(st_r + o + 4);
+  const int ids[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+  s.r[0] = r0.x; s.r[1] = r0.y; s.r[2] = r0.z; s.r[3] = r0.w;
+  s.r[4] = r1.x; s.r[5] = r1.y; s.r[6] = r1.z; s.r[7] = r1.w;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) TS::load_pre(base + (uint64_t)(uint32_t)ids[j] * kp, s.w[j]);
+}
+
+// f16 operands of one step: ratings (2p, 2p+1) share a dword, hi halves and lo
+// halves; rhs B operand by lane column (m = 0: hi(r), m = 1: lo(r), else 0).
+template <class TS>
+__device__ __forceinline__ void pre_operands(const PreStep<TS::NC>& s, uint32_t rsel,
+                                             uint32_t (&hi)[TS::NC][4], uint32_t (&lo)[TS::NC][4],
+                                             uint32_t (&rb)[4]) {
+#pragma unroll
+  for (int c = 0; c < TS::NC; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      hi[c][p] = __builtin_amdgcn_perm(s.w[2 * p + 1][c], s.w[2 * p][c], 0x05040100u);
+      lo[c][p] = __builtin_amdgcn_perm(s.w[2 * p + 1][c], s.w[2 * p][c], 0x07060302u);
+    }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) rb[p] = __builtin_amdgcn_perm(s.r[2 * p + 1], s.r[2 * p], rsel);
+}
+
+// Keep the operands where they are formed: otherwise the scheduler sinks the
+// v_perm next to their MFMAs, past the next step's loads into the same
+// registers, and the loop then carries copies of the step (waiting for its
+// loads early).
+template <class TS>
+__device__ __forceinline__ void pin_operands(uint32_t (&hi)[TS::NC][4], uint32_t (&lo)[TS::NC][4],
+                                             uint32_t (&rb)[4]) {
+#pragma unroll
+  for (int c = 0; c < TS::NC; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(hi[c][p]), "+v"(lo[c][p]));
+  if constexpr (TS::NR > 0) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) asm volatile("" : "+v"(rb[p]));
+  }
+  asm volatile("" ::: "memory");
+}
+
+template <class TS>
+__device__ __forceinline__ void pre_mfma(const uint32_t (&hi)[TS::NC][4],
+                                         const uint32_t (&lo)[TS::NC][4], const uint32_t (&rb)[4],
+                                         floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA]) {
+  split_mfma<TS>(hi, lo, acc);
+  const half8v b = as_h8(rb);
+#pragma unroll
+  for (int c = 0; c < TS::NR; ++c) {
+    accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(hi[c]), b, accb[c], 0, 0, 0);
+    accb[c] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(lo[c]), b, accb[c], 0, 0, 0);
+  }
+}
+
+// Gram tiles (acc, x 2^2ey) and rhs tiles (accb, x 2^(ey+er)) of ratings
+// [pb, pe) from the split table.  d0 = this lane's first dim (m * CN); st: 128
+// words of wave-private LDS staging.  Pipeline as gram_accumulate_split; the
+// gathers of the step after the last one read the zero row (never consumed).
+template <class TS>
+__device__ __forceinline__ void gram_accumulate_pre(
+    const int32_t* __restrict__ col, const float* __restrict__ val, int64_t pb, int64_t pe,
+    const uint32_t* __restrict__ Ysp, uint32_t kp, int zero_row, float sr, int d0,
+    floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA], int* __restrict__ st) {
+  const int lane = threadIdx.x & 63, m = lane & 15;
+  int* st_c = st;
+  uint32_t* st_r = reinterpret_cast<uint32_t*>(st + 64);
+  if (pe <= pb) return;
+  const uint32_t rsel = m == 0 ? 0x05040100u : (m == 1 ? 0x07060302u : 0x0C0C0C0Cu);
+  const uint32_t* base = Ysp + d0;
+  auto load_idx = [&](int64_t b, int& ci, float& rv) {
+    ci = zero_row;
+    rv = 0.f;
+    if (b + lane < pe) {
+      ci = col[b + lane];
+      rv = val[b + lane];
+    }
+  };
+  auto stage = [&](int ci, float rv) {
+    st_c[lane] = ci;
+    st_r[lane] = split_word(sr * rv);
+    wave_lds_sync();
+  };
+  const int nsteps = (int)((pe - pb + 31) >> 5);
+  int ci, ci_n;
+  float rv, rv_n;
+  load_idx(pb, ci, rv);
+  load_idx(pb + 64, ci_n, rv_n);
+  stage(ci, rv);
+  PreStep<TS::NC> s;
+  pre_issue<TS>(s, st_c, st_r, 0, base, kp);
+  for (int t = 0; t < nsteps; ++t) {
+    uint32_t hi[TS::NC][4], lo[TS::NC][4], rb[4];
+    pre_operands<TS>(s, rsel, hi, lo, rb);
+    pin_operands<TS>(hi, lo, rb);
+    // step t+1 = block (t+1)>>1, half (t+1)&1; a new block is staged from the
+    // pairs prefetched one block earlier
+    if (t & 1) {
+      stage(ci_n, rv_n);
+      load_idx(pb + 64 * (int64_t)((t >> 1) + 2), ci_n, rv_n);
+    }
+    pre_issue<TS>(s, st_c, st_r, (t + 1) & 1, base, kp);
+    pre_mfma<TS>(hi, lo, rb, acc, accb);
+  }
+}
+
+// rhs from the pre path's tiles: b[i*CN + gcol(c)] = C[i][0] + C[i][1] of
+// accb[c], returned in the layout of the split path's partials (lane (0, m)
+// holds dim m*CN + gcol(c), lanes with q > 0 hold 0), times `scale`.
+template <class TS>
+__device__ __forceinline__ void rhs_from_tiles(const floatx4 (&accb)[TS::NRA], float scale,
+                                               float (&bt)[TS::NRA]) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int src = (m >> 2) << 4;
+  const int rr = m & 3;
+#pragma unroll
+  for (int c = 0; c < TS::NRA; ++c) {
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = __shfl(accb[c][r] + __shfl_xor(accb[c][r], 1), src);
+    const float x = rr == 0 ? v[0] : (rr == 1 ? v[1] : (rr == 2 ? v[2] : v[3]));
+    bt[c] = (c < TS::NR && q == 0) ? x * scale : 0.f;
+  }
+}
+
+// Split table of one half-sweep's source factors (explicit only): one uint4
+// (4 dims) per thread; rows of kp = 4 << kp4_shift words; row n_src is zero.
+__global__ __launch_bounds__(256) void split_table_kernel(const float* __restrict__ Y,
+                                                          int64_t n_src, int ld, int k,
+                                                          int kp4_shift,
+                                                          const float* __restrict__ scal,
+                                                          uint4* __restrict__ Ysp) {
+  const float sy = ldexpf(1.f, split_exponent(scal[0]));
+  const int64_t total = (n_src + 1) << kp4_shift;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t row = i >> kp4_shift;
+    const int d = 4 * (int)(i & ((1 << kp4_shift) - 1));
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (row < n_src && d + 4 <= ld) v = *reinterpret_cast<const float4*>(Y + row * ld + d);
+    uint4 w;
+    w.x = d + 0 < k ? split_word(sy * v.x) : 0u;
+    w.y = d + 1 < k ? split_word(sy * v.y) : 0u;
+    w.z = d + 2 < k ? split_word(sy * v.z) : 0u;
+    w.w = d + 3 < k ? split_word(sy * v.w) : 0u;
+    Ysp[i] = w;
+  }
+}
+
+// Launch-1 task t -> heavy-row chunk or light row: the two lists interleaved
+// while both last (memory-bound Gram-only chunks beside VALU-heavy fused
+// solves), each in its own LPT order.
+__device__ __forceinline__ void decode_task(int t, int n_chunks, int n_light, int& chunk,
+                                            int& light) {
+  const int P = n_chunks < n_light ? n_chunks : n_light;
+  chunk = -1;
+  light = -1;
+  if (t < 2 * P) {
+    if (t & 1) light = t >> 1;
+    else chunk = t >> 1;
+  } else if (n_chunks > P) {
+    chunk = t - P;
+  } else {
+    light = t - P;
+  }
 }
 
 // (i, j) of register r of upper tile tt for this lane (MFMA 16x16 C layout:
@@ -833,26 +1060,25 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
   for (int c = 0; c < NRA; ++c) bt[c] = AccT(0);
 }
 
-// Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) first,
-// then whole light rows (Gram + solve fused, A never leaves the CU).
-// Gram on the split f16 MFMA (gram_accumulate_split), fp32 accumulation over a
-// task (<= chunk ratings), fp64 across the chunks of a heavy row.
-// scal[0] = max |Y| (als_absmax_kernel), scal[1] = max |rating| (implicit).
+// Launch 1 of a half-sweep: heavy-row chunks (-> fp64 partial slots) and
+// whole light rows (Gram + solve fused, A never leaves the CU), interleaved.
+// Gram on the split f16 MFMA, fp32 accumulation over a task (<= chunk
+// ratings), fp64 across the chunks of a heavy row.  scal[0] = max |Y_src|,
+// scal[1] = max |rating| (prep phase).  Explicit: Gram and rhs from the split
+// table Ysp (kp words per row, zero row `zero_row`); implicit: from Y, split in
+// registers after the per-rating confidence weight.
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ light_rows,
     const int32_t* __restrict__ chunk_row, const int64_t* __restrict__ chunk_begin,
-    const int64_t* __restrict__ chunk_end, int32_t n_chunks, const float* __restrict__ Y,
-    float* __restrict__ X, int ld, int k, float reg, float alpha,
+    const int64_t* __restrict__ chunk_end, int32_t n_chunks, int32_t n_light,
+    const float* __restrict__ Y, float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status,
-    const float* __restrict__ scal) {
+    const float* __restrict__ scal, const uint32_t* __restrict__ Ysp, int32_t kp,
+    int32_t zero_row) {
   constexpr int NT = Cfg<CN>::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
-  const int task = blockIdx.x;
-  const float wmax = IMPLICIT ? __builtin_sqrtf(alpha * scal[1]) : 1.f;
-  const int e = split_exponent(scal[0] * wmax);
-  const float sc = ldexpf(1.f, e), inv2 = ldexpf(1.f, -2 * e);
   floatx4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -860,24 +1086,41 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
 #pragma unroll
   for (int c = 0; c < CN; ++c) bt[c] = 0.f;
   int npos = 0;
+  int chunk, light;
+  decode_task(blockIdx.x, n_chunks, n_light, chunk, light);
   int64_t pb, pe;
   int row = -1;
-  if (task < n_chunks) {
-    pb = chunk_begin[task];
-    pe = chunk_end[task];
+  if (chunk >= 0) {
+    pb = chunk_begin[chunk];
+    pe = chunk_end[chunk];
   } else {
-    row = light_rows[task - n_chunks];
+    row = light_rows[light];
     pb = row_ptr[row];
     pe = row_ptr[row + 1];
   }
-  gram_accumulate_split<CN, IMPLICIT>(col, val, pb, pe, Y, ld, k, alpha, sc, acc, bt, npos,
-                                      reinterpret_cast<int*>(smem));
+  float inv2;
+  if constexpr (IMPLICIT) {
+    const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
+    inv2 = ldexpf(1.f, -2 * e);
+    gram_accumulate_split<CN, true>(col, val, pb, pe, Y, ld, k, alpha, ldexpf(1.f, e), acc, bt,
+                                    npos, reinterpret_cast<int*>(smem));
+  } else {
+    const int ey = split_exponent(scal[0]), er = split_exponent(scal[1]);
+    inv2 = ldexpf(1.f, -2 * ey);
+    floatx4 accb[CN];
+#pragma unroll
+    for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
+                                       ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
+                                       reinterpret_cast<int*>(smem));
+    rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
+  }
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
-  if (task < n_chunks) {
-    store_slot<NT, CN, float>(slots + (int64_t)task * Cfg<CN>::SLOT, tot, bt, npos);
+  if (chunk >= 0) {
+    store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt, npos);
     return;
   }
   __syncthreads();  // staging area is reused by the solve
@@ -1149,13 +1392,11 @@ __device__ __forceinline__ void wg_gram_solve_task(
     int task, const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ light_rows,
     const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
-    int32_t n_chunks, const float* __restrict__ Y, float* __restrict__ X, int ld, int k,
-    float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
-    int32_t* __restrict__ status, float* lds, const float* __restrict__ scal) {
+    int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
+    int k, float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
+    int32_t* __restrict__ status, float* lds, const float* __restrict__ scal,
+    const uint32_t* __restrict__ Ysp, int32_t kp, int32_t zero_row) {
   typedef WgTiles<R> TS;
-  const float wmax = IMPLICIT ? __builtin_sqrtf(alpha * scal[1]) : 1.f;
-  const int e = split_exponent(scal[0] * wmax);
-  const float sc = ldexpf(1.f, e), inv2 = ldexpf(1.f, -2 * e);
   floatx4 acc[TS::N];
 #pragma unroll
   for (int t = 0; t < TS::N; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1163,24 +1404,42 @@ __device__ __forceinline__ void wg_gram_solve_task(
 #pragma unroll
   for (int c = 0; c < TS::NRA; ++c) bt[c] = 0.f;
   int npos = 0;
+  int chunk, light;
+  decode_task(task, n_chunks, n_light, chunk, light);
   int64_t pb, pe;
   int row = -1;
-  if (task < n_chunks) {
-    pb = chunk_begin[task];
-    pe = chunk_end[task];
+  if (chunk >= 0) {
+    pb = chunk_begin[chunk];
+    pe = chunk_end[chunk];
   } else {
-    row = light_rows[task - n_chunks];
+    row = light_rows[light];
     pb = row_ptr[row];
     pe = row_ptr[row + 1];
   }
-  gram_accumulate_split<kWgNB, IMPLICIT, TS>(col, val, pb, pe, Y, ld, k, alpha, sc, acc, bt, npos,
-                                             reinterpret_cast<int*>(lds) + 128 * R);
+  int* st = reinterpret_cast<int*>(lds) + 128 * R;
+  float inv2;
+  if constexpr (IMPLICIT) {
+    const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
+    inv2 = ldexpf(1.f, -2 * e);
+    gram_accumulate_split<kWgNB, true, TS>(col, val, pb, pe, Y, ld, k, alpha, ldexpf(1.f, e), acc,
+                                           bt, npos, st);
+  } else {
+    const int ey = split_exponent(scal[0]), er = split_exponent(scal[1]);
+    inv2 = ldexpf(1.f, -2 * ey);
+    floatx4 accb[TS::NRA];
+#pragma unroll
+    for (int c = 0; c < TS::NRA; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gram_accumulate_pre<TS>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row, ldexpf(1.f, er),
+                            (threadIdx.x & 15) * kWgNB, acc, accb, st);
+    rhs_from_tiles<TS>(accb, ldexpf(1.f, -ey - er), bt);
+  }
 #pragma unroll
   for (int t = 0; t < TS::N; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
-  if (task < n_chunks) {
-    store_slot<TS::N, TS::NRA, float>(slots + (int64_t)task * kWgSlot + R * kWgSub, tot, bt, npos);
+  if (chunk >= 0) {
+    store_slot<TS::N, TS::NRA, float>(slots + (int64_t)chunk * kWgSlot + R * kWgSub, tot, bt,
+                                      npos);
     return;
   }
   __syncthreads();  // staging area is reused by the solve
@@ -1264,14 +1523,15 @@ __global__ __launch_bounds__(256, 2) void gram_solve_wg_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ light_rows,
     const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
-    int32_t n_chunks, const float* __restrict__ Y, float* __restrict__ X, int ld, int k,
-    float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
-    int32_t* __restrict__ status, const float* __restrict__ scal) {
+    int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
+    int k, float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
+    int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
+    int32_t kp, int32_t zero_row) {
   __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
 #define CALL(R)                                                                                 \
   wg_gram_solve_task<R, IMPLICIT>(blockIdx.x, row_ptr, col, val, light_rows, chunk_begin,      \
-                                  chunk_end, n_chunks, Y, X, ld, k, reg, alpha, yty, slots,   \
-                                  status, lds, scal)
+                                  chunk_end, n_chunks, n_light, Y, X, ld, k, reg, alpha, yty, \
+                                  slots, status, lds, scal, Ysp, kp, zero_row)
   ALS_WG_ROLES(CALL);
 #undef CALL
 }
@@ -1327,9 +1587,15 @@ static size_t slot_doubles(int k) {
 
 extern "C" {
 
-size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks) {
-  // partial slots of the heavy-row chunks, then 256 B of scale words
-  return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0)) + 256;
+static size_t solve_slots_bytes(int32_t k, int32_t n_chunks) {
+  return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
+}
+
+size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src) {
+  // partial slots of the heavy-row chunks | 256 B of scale words | split table
+  // ((n_src + 1) x k_pad words, explicit feedback)
+  return solve_slots_bytes(k, n_chunks) + 256 +
+         align_up(sizeof(uint32_t) * (size_t)als_k_pad(k) * (size_t)((n_src > 0 ? n_src : 0) + 1));
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -1350,20 +1616,26 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   ALS_REQUIRE(reg >= 0.f && alpha >= 0.f, ALS_EINVAL, "als_solve_half: reg/alpha must be >= 0");
   ALS_REQUIRE((reinterpret_cast<uintptr_t>(Y_src) & 15) == 0, ALS_EINVAL,
               "als_solve_half: Y_src must be 16-byte aligned");
-  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks), ALS_EWORKSPACE,
+  ALS_REQUIRE(n_src >= 0 && n_src < (int64_t(1) << 31), ALS_EINVAL,
+              "als_solve_half: n_src %lld not in [0, 2^31)", (long long)n_src);
+  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks, n_src), ALS_EWORKSPACE,
               "als_solve_half: workspace %zu < %zu", ws_bytes,
-              als_solve_workspace_bytes(k, n_chunks));
-  ALS_REQUIRE(n_src >= 0, ALS_EINVAL, "als_solve_half: n_src < 0");
+              als_solve_workspace_bytes(k, n_chunks, n_src));
+  ALS_REQUIRE(phases >= 1 && phases <= 7, ALS_EINVAL, "als_solve_half: phases must be in [1, 7]");
+  ALS_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, ALS_EINVAL,
+              "als_solve_half: workspace must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
   double* slots = static_cast<double*>(ws);
-  // scale words (max |Y_src|, max |rating|) after the partial slots
-  unsigned* scal_u = reinterpret_cast<unsigned*>(static_cast<char*>(ws) +
-                                                 align_up(sizeof(double) * slot_doubles(k) *
-                                                          (size_t)(n_chunks > 0 ? n_chunks : 0)));
+  // scale words (max |Y_src|, max |rating|), then the split table
+  unsigned* scal_u =
+      reinterpret_cast<unsigned*>(static_cast<char*>(ws) + solve_slots_bytes(k, n_chunks));
   const float* scal = reinterpret_cast<const float*>(scal_u);
+  uint32_t* Ysp = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scal_u) + 256);
   const int cn = cn_for_k(k);
-  ALS_REQUIRE(phases >= 1 && phases <= 3, ALS_EINVAL, "als_solve_half: phases must be 1, 2 or 3");
-  if ((phases & 1) && n_chunks + n_light > 0) {
+  const int kp = als_k_pad(k);
+  const int zero_row = (int)n_src;
+  if ((phases & 4) && n_chunks + n_light > 0) {
+    ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
     ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
     const int64_t ny = n_src * (int64_t)ld;
     if (ny > 0) {
@@ -1371,10 +1643,15 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       absmax_kernel<<<gy, 256, 0, st>>>(Y_src, ny, scal_u);
       ALS_LAUNCH_CHECK();
     }
-    if (implicit) {
-      ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
-      // every row is light or heavy: the block's ratings are val[0, row_ptr[n_light + n_heavy])
-      absmax_csr_kernel<<<1024, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
+    // every row is light or heavy: the block's ratings are val[0, row_ptr[n_light + n_heavy])
+    absmax_csr_kernel<<<1024, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
+    ALS_LAUNCH_CHECK();
+    if (!implicit) {
+      const int kp4_shift = __builtin_ctz(kp / 4);
+      const int64_t total = (n_src + 1) << kp4_shift;
+      const int gt = (int)std::min<int64_t>(4096, (total + 255) / 256);
+      split_table_kernel<<<gt, 256, 0, st>>>(Y_src, n_src, ld, k, kp4_shift, scal,
+                                             reinterpret_cast<uint4*>(Ysp));
       ALS_LAUNCH_CHECK();
     }
   }
@@ -1384,9 +1661,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   do {                                                                                            \
     if (g1)                                                                                       \
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
-                                                    chunk_begin, chunk_end, n_chunks, Y_src,      \
-                                                    X_dst, ld, k, reg, alpha, yty_packed, slots,  \
-                                                    status_dev, scal);                            \
+                                                    chunk_begin, chunk_end, n_chunks, n_light,    \
+                                                    Y_src, X_dst, ld, k, reg, alpha, yty_packed,  \
+                                                    slots, status_dev, scal, Ysp, kp, zero_row);  \
     ALS_LAUNCH_CHECK();                                                                           \
     if (g2)                                                                                       \
       reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
@@ -1398,9 +1675,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   do {                                                                                            \
     if (g1)                                                                                       \
       gram_solve_wg_kernel<IMP><<<g1, 256, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,   \
-                                                    chunk_end, n_chunks, Y_src, X_dst, ld, k,     \
-                                                    reg, alpha, yty_packed, slots, status_dev,    \
-                                                    scal);                                        \
+                                                    chunk_end, n_chunks, n_light, Y_src, X_dst,   \
+                                                    ld, k, reg, alpha, yty_packed, slots,         \
+                                                    status_dev, scal, Ysp, kp, zero_row);         \
     ALS_LAUNCH_CHECK();                                                                           \
     if (g2)                                                                                       \
       reduce_solve_wg_kernel<IMP><<<g2, 256, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \

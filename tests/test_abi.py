@@ -52,9 +52,10 @@ def test_workspace_sizes_are_monotone_and_host_only():
     L = _lib.lib()
     assert L.als_csr_workspace_bytes(1000, 10) < L.als_csr_workspace_bytes(10 ** 7, 10 ** 5)
     assert L.als_index_workspace_bytes(10, 100) < L.als_index_workspace_bytes(10, 10 ** 6)
-    assert L.als_solve_workspace_bytes(64, 0) < L.als_solve_workspace_bytes(64, 100)
-    assert L.als_solve_workspace_bytes(10, 100) < L.als_solve_workspace_bytes(64, 100)
-    assert L.als_solve_workspace_bytes(64, 100) < L.als_solve_workspace_bytes(128, 100)
+    assert L.als_solve_workspace_bytes(64, 0, 1000) < L.als_solve_workspace_bytes(64, 100, 1000)
+    assert L.als_solve_workspace_bytes(10, 100, 1000) < L.als_solve_workspace_bytes(64, 100, 1000)
+    assert L.als_solve_workspace_bytes(64, 100, 1000) < L.als_solve_workspace_bytes(128, 100, 1000)
+    assert L.als_solve_workspace_bytes(64, 100, 10) < L.als_solve_workspace_bytes(64, 100, 10 ** 6)
     assert L.als_yty_workspace_bytes(10 ** 6, 64) < L.als_yty_workspace_bytes(10 ** 6, 128)
     assert L.als_yty_workspace_bytes(10 ** 6, 64) > 0
     assert L.als_rmse_workspace_bytes(10 ** 6) > L.als_rmse_workspace_bytes(10)
@@ -73,7 +74,7 @@ def _solve_args(**over):
 @pytest.mark.parametrize("over,code", [
     (dict(k=0), -4), (dict(k=129, ld=132), -4), (dict(ld=62), -1), (dict(ld=32), -1),
     (dict(n_light=-1), -1), (dict(Y=0), -1), (dict(implicit=1), -1), (dict(reg=-1.0), -1),
-    (dict(Y=18), -1), (dict(phases=0), -1), (dict(n_src=-1), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2)])
+    (dict(Y=18), -1), (dict(phases=0), -1), (dict(phases=8), -1), (dict(n_src=-1), -1), (dict(ws=8), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2)])
 def test_solve_half_argument_errors(over, code):
     L = _lib.lib()
     rc = L.als_solve_half(*_solve_args(**over))

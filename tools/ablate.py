@@ -3,6 +3,7 @@ synthetic data (see tools/dev_ablate.hip).  Run on the GPU box:
     python tools/ablate.py
 Prints ms per launch for each mode on the item side and the user side."""
 import ctypes
+import math
 import os
 import subprocess
 import sys
@@ -24,14 +25,26 @@ def build():
                            "-std=c++17", src, "-o", SO])
 
 
+def split_table(Y, k):
+    """The explicit path's split table (as split_table_kernel): hi | lo << 16 of 2^ey * Y."""
+    ey = 14 - math.floor(math.log2(float(Y[:, :k].abs().max())))
+    t = Y[:, :k].float() * (2.0 ** ey)
+    hi = t.half()
+    lo = (t - hi.float()).half()
+    w = (hi.view(torch.int16).to(torch.int32) & 0xFFFF) | (lo.view(torch.int16).to(torch.int32) << 16)
+    z = torch.zeros((1, k), dtype=torch.int32, device=Y.device)
+    return torch.cat([w, z]).contiguous(), ey
+
+
 def main():
     if "--build" in sys.argv:
         build()
         return
     L = ctypes.CDLL(SO)
     P = ctypes.c_void_p
-    L.dev_ablate.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P, P, ctypes.c_int,
-                             ctypes.c_float, P, P]
+    F = ctypes.c_float
+    L.dev_ablate.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P, ctypes.c_int, F, F, F, P,
+                             ctypes.c_int, F, P, P]
     L.dev_ablate_wg.argtypes = L.dev_ablate.argtypes
     wg = "--wg" in sys.argv
     k = 128 if wg else 64
@@ -49,6 +62,9 @@ def main():
     for side, blk, Y, X in (("item", core.item_block, core.U, core.V),
                             ("user", core.user_block, core.V, core.U)):
         X2 = torch.empty_like(X)
+        Ysp, ey = split_table(Y, k)
+        er = 14 - math.floor(math.log2(float(blk.val.abs().max())))
+        sc = (Y.shape[0], 2.0 ** er, 2.0 ** (-2 * ey), 2.0 ** (-ey - er))
         for mode in modes:
             times = []
             for rep in range(4):
@@ -56,7 +72,7 @@ def main():
                 e0.record()
                 rc = fn(mode, blk.row_ptr.data_ptr(), blk.col.data_ptr(),
                                   blk.val.data_ptr(), blk.light_rows.data_ptr(), blk.n_light,
-                                  Y.data_ptr(), X2.data_ptr(), k, 0.1, st.data_ptr(),
+                                  Ysp.data_ptr(), *sc, X2.data_ptr(), k, 0.1, st.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)
                 e1.record()
                 torch.cuda.synchronize()

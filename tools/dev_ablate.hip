@@ -1,6 +1,7 @@
 // Dev-only ablation kernels (NOT part of libals_hip.so): the light-row path of
-// gram_solve_kernel<4,false> split into its phases, to time each on the GPU.
-//   mode 0: full (gram + tile LDL^T on MFMA)
+// gram_solve_kernel<4,false> (explicit, pre-split Gram) split into its phases,
+// to time each on the GPU.
+//   mode 0: full (gram + panel LDL^T)
 //   mode 1: gram only (accumulate, then write a checksum so nothing is dead)
 //   mode 2: solve only (synthetic SPD matrix in registers, tile LDL^T)
 //   mode 5: half the workgroups gram-only, half solve-only (overlap test)
@@ -18,28 +19,31 @@ __global__ __launch_bounds__(64, 3) void ablate_kernel(const int64_t* __restrict
                                                        const int32_t* __restrict__ col,
                                                        const float* __restrict__ val,
                                                        const int32_t* __restrict__ rows, int n,
-                                                       const float* __restrict__ Y,
-                                                       float* __restrict__ X, int ld, float reg,
-                                                       int32_t* __restrict__ status) {
+                                                       const uint32_t* __restrict__ Ysp,
+                                                       int zero_row, float sr, float inv2,
+                                                       float invb, float* __restrict__ X, int ld,
+                                                       float reg, int32_t* __restrict__ status) {
   constexpr int CN = 4, NT = Cfg<CN>::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int row = rows[blockIdx.x];
   const int lane = threadIdx.x;
   float tot[NT][4], bt[CN];
   zero_acc<NT, CN, float>(tot, bt);
-  int npos = 0;
   const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
   bool gram = MODE == 0 || MODE == 1 || (MODE == 5 && (blockIdx.x & 1));
   if (gram) {
-    floatx4 acc[NT];
+    floatx4 acc[NT], accb[CN];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-    gram_accumulate_split<CN, false>(col, val, pb, pe, Y, ld, 64, 0.f, 1.f, acc, bt, npos,
-                                     reinterpret_cast<int*>(smem));
+#pragma unroll
+    for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, 64u, zero_row, sr, (lane & 15) * CN,
+                                       acc, accb, reinterpret_cast<int*>(smem));
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r];
+      for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
+    rhs_from_tiles<FullTiles<CN>>(accb, invb, bt);
     __syncthreads();
   } else {
     // synthetic SPD system: small off-diagonals, diagonal from regularisation
@@ -69,19 +73,30 @@ __device__ __forceinline__ void ablate_wg_task(const int64_t* __restrict__ row_p
                                                const int32_t* __restrict__ col,
                                                const float* __restrict__ val,
                                                const int32_t* __restrict__ rows,
-                                               const float* __restrict__ Y, float* __restrict__ X,
-                                               int ld, float reg, int32_t* __restrict__ status,
-                                               float* lds) {
+                                               const uint32_t* __restrict__ Ysp, int zero_row,
+                                               float sr, float inv2, float invb,
+                                               float* __restrict__ X, int ld, float reg,
+                                               int32_t* __restrict__ status, float* lds) {
   typedef WgTiles<R> TS;
   const int lane = threadIdx.x & 63;
   float tot[TS::N][4], bt[TS::NRA];
   zero_acc<TS::N, TS::NRA, float>(tot, bt);
-  int npos = 0;
   const int row = rows[blockIdx.x];
   const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
   if (MODE != 2) {
-    gram_accumulate<kWgNB, false, false, float, TS>(col, val, pb, pe, Y, ld, 128, 0.f, tot, bt,
-                                                    npos);
+    floatx4 acc[TS::N], accb[TS::NRA];
+#pragma unroll
+    for (int t = 0; t < TS::N; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < TS::NRA; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gram_accumulate_pre<TS>(col, val, pb, pe, Ysp, 128u, zero_row, sr, (lane & 15) * kWgNB, acc,
+                            accb, reinterpret_cast<int*>(lds) + 128 * R);
+#pragma unroll
+    for (int t = 0; t < TS::N; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
+    rhs_from_tiles<TS>(accb, invb, bt);
+    __syncthreads();
   } else {
 #pragma unroll
     for (int t = 0; t < TS::N; ++t)
@@ -108,26 +123,33 @@ __global__ __launch_bounds__(256, 2) void ablate_wg_kernel(const int64_t* __rest
                                                            const int32_t* __restrict__ col,
                                                            const float* __restrict__ val,
                                                            const int32_t* __restrict__ rows,
-                                                           const float* __restrict__ Y,
-                                                           float* __restrict__ X, int ld,
-                                                           float reg,
+                                                           const uint32_t* __restrict__ Ysp,
+                                                           int zero_row, float sr, float inv2,
+                                                           float invb, float* __restrict__ X,
+                                                           int ld, float reg,
                                                            int32_t* __restrict__ status) {
   __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wv == 0) ablate_wg_task<0, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
-  else if (wv == 1) ablate_wg_task<1, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
-  else if (wv == 2) ablate_wg_task<2, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
-  else ablate_wg_task<3, MODE>(row_ptr, col, val, rows, Y, X, ld, reg, status, lds);
+#define T(R) \
+  ablate_wg_task<R, MODE>(row_ptr, col, val, rows, Ysp, zero_row, sr, inv2, invb, X, ld, reg, status, lds)
+  if (wv == 0) T(0);
+  else if (wv == 1) T(1);
+  else if (wv == 2) T(2);
+  else T(3);
+#undef T
 }
 
 }  // namespace als
 
 extern "C" int dev_ablate(int mode, const int64_t* row_ptr, const int32_t* col, const float* val,
-                          const int32_t* rows, int n, const float* Y, float* X, int ld, float reg,
-                          int32_t* status, void* stream) {
+                          const int32_t* rows, int n, const uint32_t* Ysp, int zero_row, float sr,
+                          float inv2, float invb, float* X, int ld, float reg, int32_t* status,
+                          void* stream) {
   using namespace als;
   hipStream_t st = (hipStream_t)stream;
-#define L(M) ablate_kernel<M><<<n, 64, 0, st>>>(row_ptr, col, val, rows, n, Y, X, ld, reg, status)
+#define L(M)                                                                                 \
+  ablate_kernel<M><<<n, 64, 0, st>>>(row_ptr, col, val, rows, n, Ysp, zero_row, sr, inv2, invb, \
+                                     X, ld, reg, status)
   switch (mode) {
     case 0: L(0); break;
     case 1: L(1); break;
@@ -140,11 +162,14 @@ extern "C" int dev_ablate(int mode, const int64_t* row_ptr, const int32_t* col, 
 }
 
 extern "C" int dev_ablate_wg(int mode, const int64_t* row_ptr, const int32_t* col,
-                             const float* val, const int32_t* rows, int n, const float* Y,
-                             float* X, int ld, float reg, int32_t* status, void* stream) {
+                             const float* val, const int32_t* rows, int n, const uint32_t* Ysp,
+                             int zero_row, float sr, float inv2, float invb, float* X, int ld,
+                             float reg, int32_t* status, void* stream) {
   using namespace als;
   hipStream_t st = (hipStream_t)stream;
-#define L(M) ablate_wg_kernel<M><<<n, 256, 0, st>>>(row_ptr, col, val, rows, Y, X, ld, reg, status)
+#define L(M)                                                                                   \
+  ablate_wg_kernel<M><<<n, 256, 0, st>>>(row_ptr, col, val, rows, Ysp, zero_row, sr, inv2, invb, \
+                                         X, ld, reg, status)
   switch (mode) {
     case 0: L(0); break;
     case 1: L(1); break;

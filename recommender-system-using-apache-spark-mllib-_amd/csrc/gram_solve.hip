@@ -775,15 +775,6 @@ __device__ __forceinline__ double readlane_t(double v, int l) { return readlane_
 // LDS (floats): tile slots NT x 288 (16 columns, stride 18: 8-B aligned, at
 // most 2-way conflicts on the MFMA operand reads) | z, d, x 3 x 16 NB.
 // ---------------------------------------------------------------------------
-// This lane's id, opaque to the optimizer: per-pivot lane masks are then
-// computed where they are used instead of being hoisted into (and spilling)
-// scalar registers across the unrolled pivot loops.
-__device__ __forceinline__ int lane_opaque() {
-  int l = threadIdx.x & 63;
-  asm volatile("" : "+v"(l));
-  return l;
-}
-
 template <int CN>
 struct PanelLds {
   static constexpr int NB = CN, NT = CN * (CN + 1) / 2, CS = 18;  // column stride
@@ -814,6 +805,56 @@ __device__ __forceinline__ void regularise_f32(floatx4 (&A)[Cfg<CN>::NT], float 
       }
       ++tt;
     }
+  }
+}
+
+// x on lanes above P, 0 on lanes <= P.  The lane mask comes from the scalar
+// unit (all-ones shifted left by P + 1), so the gate costs one VALU op.
+template <int P>
+__device__ __forceinline__ float gate_above(float x) {
+  float r;
+  uint64_t m;
+  asm volatile("s_lshl_b64 %1, -1, %2\n\ts_nop 0\n\tv_cndmask_b32_e64 %0, 0, %3, %1"
+               : "=v"(r), "=&s"(m)
+               : "i"(P + 1), "v"(x));
+  return r;
+}
+
+// Lane P of v replaced by the uniform value s (one v_writelane; the s_nop
+// covers an SGPR just written by v_readlane).
+template <int P>
+__device__ __forceinline__ float put_lane(float v, float s) {
+  asm volatile("s_nop 1\n\tv_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(s), "i"(P));
+  return v;
+}
+
+// Pivot p's broadcasts from lane p: a[i] = R_p[i] for i >= p (a[p] = the pivot
+// d) and bp = rb_p.  The uniform-index ds_bpermute becomes one v_readlane per
+// value (measured: the LDS round trip on this serial chain is slower); all are
+// issued before their FMAs, into distinct SGPRs, so no SGPR-hazard s_nop pads
+// the updates, which then run two rows per v_pk_fma_f32 with an SGPR pair.
+template <int N>
+__device__ __forceinline__ void pivot_broadcast(const float (&R)[N], float rb, int p,
+                                                float (&a)[N], float& bp) {
+  const int addr = p << 2;
+#pragma unroll
+  for (int i = p; i < N; ++i)
+    a[i] = __builtin_bit_cast(float,
+                              __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, R[i])));
+  bp = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, rb)));
+}
+
+// R[i] -= a[i] * f for i > p, two rows per v_pk_fma_f32 (for even p the pair
+// (p, p+1) is updated too; the caller then overwrites R[p]).
+template <int N>
+__device__ __forceinline__ void pivot_update(float (&R)[N], const float (&a)[N], int p, float f) {
+  const float2v nf = {-f, -f};
+#pragma unroll
+  for (int i = (p + 1) & ~1; i < N; i += 2) {
+    const float2v r = __builtin_elementwise_fma((float2v){a[i], a[i + 1]}, nf,
+                                                (float2v){R[i], R[i + 1]});
+    R[i] = r[0];
+    R[i + 1] = r[1];
   }
 }
 
@@ -876,7 +917,7 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
 #pragma unroll
   for (int c = 0; c < CN; ++c)
     if (q == c) rb = bq[c];
-  bool ok = true;
+  bool okl = true;  // this lane: every pivot of its diagonal lane was > 0
   static_for<NB>([&](auto Kc) {
     constexpr int K = decltype(Kc)::value;
     constexpr int NCOL = 16 * (NB - K);
@@ -900,20 +941,20 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     }
     // (b) 16 pivots over the whole panel (diag LDL^T + TRSM + rhs forward)
     float myd = 1.f;
-#pragma unroll
-    for (int p = 0; p < 16; ++p) {
-      const float d = readlane_t(R[p], p);
-      ok = ok && (d > 0.f);
+    static_for<16>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      float a[16];
+      float bp;
+      pivot_broadcast<16>(R, rb, p, a, bp);
+      const float d = a[p];
       const float rd = rcp_t(d);
-      const float bp = readlane_t(rb, p);
-      const int lo = lane_opaque();
-      const float f = lo > p ? R[p] * rd : 0.f;  // U[p][t]; 0 below the diagonal
+      const float f = gate_above<p>(R[p] * rd);  // U[p][t]; 0 below the diagonal
       rb = fmaf(-f, bp, rb);
-#pragma unroll
-      for (int i = p + 1; i < 16; ++i) R[i] = fmaf(-readlane_t(R[i], p), f, R[i]);
+      pivot_update<16>(R, a, p, f);
       R[p] = f;
-      if (lo == p) myd = d;
-    }
+      myd = put_lane<p>(myd, d);
+    });
+    okl = okl && (myd > 0.f);  // lanes >= 16 keep myd = 1; NaN pivots fail
     // (c) U columns -> tile slots (block row K); z_K, D_K
     if (col_ok) {
 #pragma unroll
@@ -949,6 +990,7 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     }
   });
   wave_lds_sync();
+  const bool ok = __ballot(!okl) == 0;
   // (e) back substitution
   block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);
   // (f) un-permute: dim d = i*CN + K  <->  Xv[K*16 + i]
@@ -1252,7 +1294,7 @@ __device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], floa
   float* Xv = lds + Lo::X;
   float* RBv = lds + Lo::RB;
   auto slot = [&](int I, int J) { return lds + Lo::T + tile_index(NB, I, J) * 16 * CS; };
-  bool ok = true;
+  bool okl = true;  // this lane: every pivot of its diagonal lane was > 0
   static_for<NB>([&](auto Kc) {
     constexpr int K = decltype(Kc)::value;
     // (a) owners: block row K -> column-major slots
@@ -1281,20 +1323,20 @@ __device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], floa
       }
       float rb = RBv[16 * Jl + m];
       float myd = 1.f;
-#pragma unroll
-      for (int p = 0; p < 16; ++p) {
-        const float d = readlane_t(R16[p], p);
-        ok = ok && (d > 0.f);
+      static_for<16>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        float a[16];
+        float bp;
+        pivot_broadcast<16>(R16, rb, p, a, bp);
+        const float d = a[p];
         const float rd = rcp_t(d);
-        const float bp = readlane_t(rb, p);
-        const int lo = lane_opaque();
-        const float f = lo > p ? R16[p] * rd : 0.f;
+        const float f = gate_above<p>(R16[p] * rd);
         rb = fmaf(-f, bp, rb);
-#pragma unroll
-        for (int i = p + 1; i < 16; ++i) R16[i] = fmaf(-readlane_t(R16[i], p), f, R16[i]);
+        pivot_update<16>(R16, a, p, f);
         R16[p] = f;
-        if (lo == p) myd = d;
-      }
+        myd = put_lane<p>(myd, d);
+      });
+      okl = okl && (myd > 0.f);  // lanes >= 16 keep myd = 1; NaN pivots fail
       if (col_ok && (q > 0 || R == 0)) {
 #pragma unroll
         for (int c2 = 0; c2 < 8; ++c2)
@@ -1328,6 +1370,7 @@ __device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], floa
       });
     }
   });
+  const bool ok = __ballot(!okl) == 0;
   if constexpr (R == 0) {
     // (d) back substitution
     block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);

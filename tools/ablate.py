@@ -16,7 +16,7 @@ import _pkgload  # noqa: E402
 _pkgload.load()
 from als_mi355x import datasets as D, engine as E  # noqa: E402
 
-SO = os.path.join(ROOT, "tools", "libals_dev.so")
+SO = os.environ.get("ALS_DEV_SO", os.path.join(ROOT, "tools", "libals_dev.so"))
 
 
 def build():

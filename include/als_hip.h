@@ -156,10 +156,14 @@ int als_rmse_partial(const int32_t* u, const int32_t* i, const float* r, int64_t
  *      predictAll + takeOrdered(20) flow at RecommenderSystem.py:229-247) -- */
 
 /* For each of the n_q query rows of Q, the `top` rows of V with the largest
- * fp32 score <q, v>, ordered by score descending then index ascending.
+ * score <q, v>, ordered by score descending then index ascending.
  * idx_out[n_q*top] (dense row index of V, -1 when n_v < top), score_out[n_q*top].
- * k <= 64, top <= 256.  The n_q x n_v score matrix is never materialised. */
-size_t als_topk_workspace_bytes(int64_t n_q, int32_t top);
+ * Scores: fp32-grade products on the f16 matrix cores (q and v split into f16
+ * hi + lo after power-of-two scaling, ~2^-21 relative to |q||v|); fp32 MFMA when
+ * the lists need more LDS than the split kernel leaves.  k <= 128, top <= 256
+ * (<= 253 at k > 64: LDS).  The n_q x n_v score matrix is never materialised.
+ * Workspace (16-byte aligned): scale words + the split copy of V. */
+size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top);
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v,
              int32_t ld, int32_t k, int32_t top,
              int32_t* idx_out, float* score_out, void* ws, size_t ws_bytes, void* stream);

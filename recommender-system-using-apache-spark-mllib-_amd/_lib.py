@@ -50,7 +50,7 @@ SIGNATURES = {
     "als_rmse_workspace_bytes": (SZ, [I64]),
     "als_rmse_partial": (ctypes.c_int, [P, P, P, I64, P, I32, P, I32, P, P, I32, I32, P, P, SZ,
                                         P]),
-    "als_topk_workspace_bytes": (SZ, [I64, I32]),
+    "als_topk_workspace_bytes": (SZ, [I64, I64, I32, I32]),
     "als_topk": (ctypes.c_int, [P, I64, P, I64, I32, I32, I32, P, P, P, SZ, P]),
 }
 

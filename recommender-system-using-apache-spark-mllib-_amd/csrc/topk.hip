@@ -7,20 +7,76 @@
 // reference's own top-k is `predictAll` over one user's unrated movies then
 // `takeOrdered(20, key=-pred)` (RecommenderSystem.py:229-247).
 //
-// Workgroup = 4 wavefronts = 64 query rows (16 per wave).  The workgroup
+// Scores on the f16 matrix cores with fp32-grade products (the split scheme
+// of the Gram in gram_solve.hip): q and v are scaled by powers of two (from
+// max |Q| and max |V|) and carried as f16 hi + lo, hi = f16_rn(t),
+// lo = f16_rn(t - hi); <q, v> = hi.hi + hi.lo + lo.hi accumulated in fp32 by
+// v_mfma_f32_16x16x32_f16 (~2^-21 relative to |q||v| per product, below the
+// rounding of Spark's fp32 sgemm).  V is split once per call into f16 planes
+// (topk_split_table_kernel: row r = [hi of dims 0..KQ) | lo of dims 0..KQ)]),
+// so a staged tile row is copied as is and every B operand is one
+// ds_read_b128.  The query rows are split in registers once per workgroup.
+//
+// Workgroup = 4 wavefronts x RG row groups = 64 RG query rows.  The workgroup
 // sweeps V in 64-row tiles staged in LDS (rows padded by 16 B: the 16 lanes
-// of a row-group read 16 distinct bank slots).  Per tile each wave computes a
-// 16 x 64 score block with v_mfma_f32_16x16x4_f32 (fp32 in, fp32 accumulate:
-// Spark's ml path is fp32 sgemm too), then filters it against each row's
-// current k-th best (score, index) and inserts the rare survivors into a
-// sorted list in LDS with a wave-cooperative insertion.  Order: score
-// descending, ties by ascending index (the build's deterministic tie rule,
-// SURVEY Appendix A.6).
+// of a row-group read distinct bank slots); the next tile's global loads are
+// in flight while the current one is scored.  Per tile each wave computes
+// RG 16 x 64 score blocks, then filters each against its rows' current k-th
+// best (score, index) and inserts the rare survivors into a sorted list in
+// LDS with a wave-cooperative insertion.  Order: score descending, ties by
+// ascending index (the build's deterministic tie rule).
+// Scores are compared in the scaled domain (exact: powers of two) and
+// unscaled on output.
+//
+// When the split kernel's lists do not fit the LDS, topk_kernel — the same
+// structure with fp32 MFMA (v_mfma_f32_16x16x4_f32) straight from the fp32
+// rows and 64 query rows per workgroup — is used.
 #include "als_common.h"
+
+#include <algorithm>
 
 namespace als {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+namespace {
+
+typedef _Float16 tk_half8 __attribute__((ext_vector_type(8)));
+
+// Power-of-two scale exponent: the largest |t| of the operand lands in [2^14, 2^15).
+__device__ __forceinline__ int tk_split_exponent(float m) {
+  if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+  int e = 14 - ilogbf(m);
+  return e < -60 ? -60 : (e > 60 ? 60 : e);
+}
+
+__device__ __forceinline__ void tk_split(float t, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)t;  // round to nearest
+  lo = (_Float16)(t - (float)hi);
+}
+
+// max |x| over n floats -> *out (ordered uint bits; *out zeroed beforehand).
+__global__ __launch_bounds__(256) void tk_absmax_kernel(const float* __restrict__ x, int64_t n,
+                                                        unsigned* __restrict__ out) {
+  float m = 0.f;
+  const int64_t n4 = n >> 2;
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = x4[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = fmaxf(m, fabsf(x[4 * n4 + threadIdx.x]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(out, __float_as_uint(m));  // NaN-free non-negative floats order as uints
+  }
+}
+
+}  // namespace
 
 constexpr int kTopkMax = 256;
 constexpr int kLdsBytes = 160 * 1024;  // per CU on gfx950 (one workgroup may use it all)
@@ -29,6 +85,239 @@ __device__ __forceinline__ bool beats(float s1, int i1, float s2, int i2) {
   return s1 > s2 || (s1 == s2 && i1 < i2);
 }
 
+// Offer one 16 x 16 score block to the sorted per-row lists: acc[r] = score of
+// list row slot0 + 4q + r against V row ibase + m.  Candidates that beat their
+// row's current k-th (score, index) are inserted one at a time by the whole
+// wave (rank by ballot, shift, insert), lowest lane first.
+__device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_t n_v,
+                                           float (&ts)[4], int (&ti)[4], float* __restrict__ ls,
+                                           int* __restrict__ li, int* __restrict__ len, int slot0,
+                                           int top) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int vidx = ibase + m;
+  const bool vin = (int64_t)vidx < n_v;
+  int pend = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (vin && beats(acc[r], vidx, ts[r], ti[r])) pend |= 1 << r;
+  uint64_t any = __ballot(pend != 0);
+  while (any) {
+    const int L = __builtin_ctzll(any);
+    const int myr = pend ? __builtin_ctz(pend) : 0;
+    const float mys = myr == 0 ? acc[0] : (myr == 1 ? acc[1] : (myr == 2 ? acc[2] : acc[3]));
+    const int rL = __builtin_amdgcn_readlane(myr, L);
+    const float sc =
+        __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mys), L));
+    const int itm = ibase + (L & 15);
+    const int slot = slot0 + 4 * (L >> 4) + rL;  // list row within the workgroup
+    float* lsr = ls + slot * top;
+    int* lir = li + slot * top;
+    const int n = len[slot];
+    // rank = number of entries that beat the candidate
+    int pos = 0;
+    for (int e0 = 0; e0 < n; e0 += 64) {
+      const int e = e0 + lane;
+      const bool bt = e < n && beats(lsr[e], lir[e], sc, itm);
+      pos += __popcll(__ballot(bt));
+    }
+    if (pos < top) {
+      const int newn = n + 1 < top ? n + 1 : top;
+      float hs[kTopkMax / 64];
+      int hi[kTopkMax / 64];
+#pragma unroll
+      for (int j = 0; j < kTopkMax / 64; ++j) {
+        const int e = 64 * j + lane;
+        if (e > pos && e < newn) {
+          hs[j] = lsr[e - 1];
+          hi[j] = lir[e - 1];
+        }
+      }
+      // reads of the shifted entries land before any lane writes (compiler + HW order)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < kTopkMax / 64; ++j) {
+        const int e = 64 * j + lane;
+        if (e > pos && e < newn) {
+          lsr[e] = hs[j];
+          lir[e] = hi[j];
+        }
+      }
+      if (lane == 0) {
+        lsr[pos] = sc;
+        lir[pos] = itm;
+        len[slot] = newn;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (newn == top) {
+        const float ks = lsr[top - 1];
+        const int ki = lir[top - 1];
+        if (q == (L >> 4)) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (r == rL) {
+              ts[r] = ks;
+              ti[r] = ki;
+            }
+        }
+      }
+    }
+    if (lane == L) pend &= ~(1 << rL);
+    // drop pending candidates of that row that no longer beat its threshold
+    if (q == (L >> 4)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (r == rL && (pend >> r & 1) && !beats(acc[r], vidx, ts[r], ti[r])) pend &= ~(1 << r);
+    }
+    any = __ballot(pend != 0);
+  }
+}
+
+// Write the lists of rows slot0 .. slot0+15 (one wave) to the outputs.
+__device__ __forceinline__ void topk_write(const float* __restrict__ ls, const int* __restrict__ li,
+                                           const int* __restrict__ len, int slot0, int64_t qbase,
+                                           int64_t n_q, int top, float unscale,
+                                           int32_t* __restrict__ idx_out,
+                                           float* __restrict__ score_out) {
+  const int lane = threadIdx.x & 63;
+  for (int rr = 0; rr < 16; ++rr) {
+    const int slot = slot0 + rr;
+    const int64_t row = qbase + slot;
+    if (row >= n_q) break;
+    const int n = len[slot];
+    for (int e = lane; e < top; e += 64) {
+      idx_out[row * top + e] = e < n ? li[slot * top + e] : -1;
+      score_out[row * top + e] = e < n ? ls[slot * top + e] * unscale : -__builtin_inff();
+    }
+  }
+}
+
+// V -> split planes, row r = [hi(sv v[0..KQ)) | lo(sv v[0..KQ))] (f16), dims >= k zero.
+__global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __restrict__ V,
+                                                               int64_t n_v, int ld, int k,
+                                                               int kq_shift,
+                                                               const float* __restrict__ scal,
+                                                               _Float16* __restrict__ out) {
+  const float sv = ldexpf(1.f, tk_split_exponent(scal[1]));
+  const int kq = 1 << kq_shift;
+  const int64_t total = n_v << kq_shift;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t r = e >> kq_shift;
+    const int d = (int)(e & (kq - 1));
+    const float t = d < k ? sv * V[r * ld + d] : 0.f;
+    _Float16 h, l;
+    tk_split(t, h, l);
+    out[2 * (r << kq_shift) + d] = h;
+    out[2 * (r << kq_shift) + kq + d] = l;
+  }
+}
+
+// Split-f16 scores.  NK = KQ / 32 MFMA k-steps (KQ = k padded to 32, 64 or 128);
+// RG query-row groups of 64 per workgroup.  scal[0] = max |Q|, scal[1] = max |V|.
+template <int NK, int RG>
+__global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
+                                                         const uint4* __restrict__ Vsp,
+                                                         int64_t n_v, int ld, int k, int top,
+                                                         const float* __restrict__ scal,
+                                                         int32_t* __restrict__ idx_out,
+                                                         float* __restrict__ score_out) {
+  constexpr int KQ = 32 * NK;
+  constexpr int RW = KQ / 4;          // uint4 per split row (KQ hi + KQ lo halves)
+  constexpr int RS = RW + 1;          // LDS row stride in uint4 (16-B pad)
+  constexpr int PER = 64 * RW / 256;  // staged uint4 per thread per tile
+  extern __shared__ uint4 smem_u4[];
+  uint4* tile = smem_u4;                                 // [64][RS]
+  float* ls = reinterpret_cast<float*>(tile + 64 * RS);  // [64 RG rows][top] scores
+  int* li = reinterpret_cast<int*>(ls + 64 * RG * top);  // [64 RG rows][top] indices
+  int* len = li + 64 * RG * top;                         // [64 RG]
+
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int64_t qbase = (int64_t)blockIdx.x * 64 * RG;
+  const int eu = tk_split_exponent(scal[0]), ev = tk_split_exponent(scal[1]);
+  const float su = ldexpf(1.f, eu), unscale = ldexpf(1.f, -eu - ev);
+
+  // A operands: group g, k-step s, lane (q, m): dims 32s + 8q .. +7 of query row
+  // qbase + 64g + 16w + m, as hi and lo halves.
+  tk_half8 ah[RG][NK], al[RG][NK];
+#pragma unroll
+  for (int g = 0; g < RG; ++g) {
+    const int64_t row = qbase + 64 * g + 16 * w + m;
+    const bool ok = row < n_q;
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int d = 32 * s + 8 * q + j;
+        const float t = (ok && d < k) ? su * Q[row * ld + d] : 0.f;
+        _Float16 h, l;
+        tk_split(t, h, l);
+        ah[g][s][j] = h;
+        al[g][s][j] = l;
+      }
+    }
+  }
+  if (threadIdx.x < 64 * RG) len[threadIdx.x] = 0;
+  float ts[RG][4];
+  int ti[RG][4];
+#pragma unroll
+  for (int g = 0; g < RG; ++g)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ts[g][r] = -__builtin_inff();
+      ti[g][r] = 0x7fffffff;
+    }
+
+  uint4 pre[PER];
+  auto fetch = [&](int64_t vb) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = threadIdx.x + 256 * e;
+      const int64_t vrow = vb + x / RW;
+      pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  fetch(0);
+  for (int64_t vb = 0; vb < n_v; vb += 64) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = threadIdx.x + 256 * e;
+      tile[(x / RW) * RS + x % RW] = pre[e];
+    }
+    __syncthreads();
+    if (vb + 64 < n_v) fetch(vb + 64);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      // B operand: lane (q, m) holds dims 32s + 8q .. +7 of V row vb + 16c + m
+      const uint4* tb = tile + (16 * c + m) * RS;
+      floatx4 acc[RG];
+#pragma unroll
+      for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < NK; ++s) {
+        const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+        const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[KQ / 8 + 4 * s + q]);
+#pragma unroll
+        for (int g = 0; g < RG; ++g) {
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bl, acc[g], 0, 0, 0);
+          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[g][s], bh, acc[g], 0, 0, 0);
+        }
+      }
+      // acc[g][r] = scaled score(row 64g + 16w + 4q + r, V row vb + 16c + m)
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+        topk_offer(acc[g], (int)(vb + 16 * c), n_v, ts[g], ti[g], ls, li, len, 64 * g + 16 * w,
+                   top);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int g = 0; g < RG; ++g)
+    topk_write(ls, li, len, 64 * g + 16 * w, qbase, n_q, top, unscale, idx_out, score_out);
+}
+
+// fp32 scores (used when the split kernel's lists do not fit the LDS).
 template <int CN>
 __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ Q, int64_t n_q,
                                                    const float* __restrict__ V, int64_t n_v,
@@ -99,96 +388,11 @@ __global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ Q, 
         acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s4 + 3], b4.w, acc, 0, 0, 0);
       }
       // acc[r] = score(row 16w + 4q + r, V row vb + 16c + m)
-      const int vidx = (int)(vb + 16 * c + m);
-      const bool vin = (vb + 16 * c + m) < n_v;
-      int pend = 0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (vin && beats(acc[r], vidx, ts[r], ti[r])) pend |= 1 << r;
-      uint64_t any = __ballot(pend != 0);
-      while (any) {
-        const int L = __builtin_ctzll(any);
-        const int myr = pend ? __builtin_ctz(pend) : 0;
-        const float mys = myr == 0 ? acc[0] : (myr == 1 ? acc[1] : (myr == 2 ? acc[2] : acc[3]));
-        const int rL = __builtin_amdgcn_readlane(myr, L);
-        const float sc = __builtin_bit_cast(float,
-                                            __builtin_amdgcn_readlane(__builtin_bit_cast(int, mys), L));
-        const int itm = (int)(vb + 16 * c + (L & 15));
-        const int slot = 16 * w + 4 * (L >> 4) + rL;  // list row within the workgroup
-        float* lsr = ls + slot * top;
-        int* lir = li + slot * top;
-        const int n = len[slot];
-        // rank = number of entries that beat the candidate
-        int pos = 0;
-        for (int e0 = 0; e0 < n; e0 += 64) {
-          const int e = e0 + lane;
-          const bool bt = e < n && beats(lsr[e], lir[e], sc, itm);
-          pos += __popcll(__ballot(bt));
-        }
-        if (pos < top) {
-          const int newn = n + 1 < top ? n + 1 : top;
-          float hs[kTopkMax / 64];
-          int hi[kTopkMax / 64];
-#pragma unroll
-          for (int j = 0; j < kTopkMax / 64; ++j) {
-            const int e = 64 * j + lane;
-            if (e > pos && e < newn) {
-              hs[j] = lsr[e - 1];
-              hi[j] = lir[e - 1];
-            }
-          }
-          // reads of the shifted entries land before any lane writes (compiler + HW order)
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-          for (int j = 0; j < kTopkMax / 64; ++j) {
-            const int e = 64 * j + lane;
-            if (e > pos && e < newn) {
-              lsr[e] = hs[j];
-              lir[e] = hi[j];
-            }
-          }
-          if (lane == 0) {
-            lsr[pos] = sc;
-            lir[pos] = itm;
-            len[slot] = newn;
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (newn == top) {
-            const float ks = lsr[top - 1];
-            const int ki = lir[top - 1];
-            if (q == (L >> 4)) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (r == rL) {
-                  ts[r] = ks;
-                  ti[r] = ki;
-                }
-            }
-          }
-        }
-        if (lane == L) pend &= ~(1 << rL);
-        // drop pending candidates of that row that no longer beat its threshold
-        if (q == (L >> 4)) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (r == rL && (pend >> r & 1) && !beats(acc[r], vidx, ts[r], ti[r])) pend &= ~(1 << r);
-        }
-        any = __ballot(pend != 0);
-      }
+      topk_offer(acc, (int)(vb + 16 * c), n_v, ts, ti, ls, li, len, 16 * w, top);
     }
   }
   __syncthreads();
-  // write each wave's 16 lists
-  for (int rr = 0; rr < 16; ++rr) {
-    const int slot = 16 * w + rr;
-    const int64_t row = qbase + slot;
-    if (row >= n_q) break;
-    const int n = len[slot];
-    for (int e = lane; e < top; e += 64) {
-      idx_out[row * top + e] = e < n ? li[slot * top + e] : -1;
-      score_out[row * top + e] = e < n ? ls[slot * top + e] : -__builtin_inff();
-    }
-  }
+  topk_write(ls, li, len, 16 * w, qbase, n_q, top, 1.f, idx_out, score_out);
 }
 
 static size_t topk_lds_bytes(int cn, int top) {
@@ -197,23 +401,37 @@ static size_t topk_lds_bytes(int cn, int top) {
          sizeof(int) * 64;
 }
 
+static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
+
+static size_t topk_split_lds_bytes(int kq, int rg, int top) {
+  return 16 * 64 * (size_t)(kq / 4 + 1) + (sizeof(float) + sizeof(int)) * 64 * (size_t)rg * top +
+         sizeof(int) * 64 * (size_t)rg;
+}
+
+// Row groups per workgroup of the split kernel (0: its lists do not fit the LDS).
+static int topk_split_rg(int k, int top) {
+  const int kq = topk_kq(k);
+  if (topk_split_lds_bytes(kq, 2, top) <= (size_t)kLdsBytes) return 2;
+  if (topk_split_lds_bytes(kq, 1, top) <= (size_t)kLdsBytes) return 1;
+  return 0;
+}
+
 }  // namespace als
 
 using namespace als;
 
 extern "C" {
 
-size_t als_topk_workspace_bytes(int64_t n_q, int32_t top) {
+size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top) {
   (void)n_q;
   (void)top;
-  return 0;
+  // 256 B of scale words, then the split planes of V (2 x KQ halves per row)
+  return 256 + align_up(4 * (size_t)topk_kq(k) * (size_t)(n_v > 0 ? n_v : 0));
 }
 
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t ld, int32_t k,
              int32_t top, int32_t* idx_out, float* score_out, void* ws, size_t ws_bytes,
              void* stream) {
-  (void)ws;
-  (void)ws_bytes;
   ALS_REQUIRE(k >= 1 && k <= 128, ALS_EUNSUPPORTED, "als_topk: rank %d not in [1, 128]", k);
   ALS_REQUIRE(ld >= k && ld % 4 == 0, ALS_EINVAL, "als_topk: bad ld");
   ALS_REQUIRE(top >= 1 && top <= kTopkMax, ALS_EUNSUPPORTED, "als_topk: top %d not in [1, %d]",
@@ -224,10 +442,12 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   ALS_REQUIRE(Q && V && idx_out && score_out, ALS_EINVAL, "als_topk: null pointer");
   hipStream_t st = as_stream(stream);
   const int cn = k <= 16 ? 1 : (k <= 32 ? 2 : (k <= 64 ? 4 : 8));
-  const size_t lds = topk_lds_bytes(cn, top);
-  ALS_REQUIRE(lds <= kLdsBytes, ALS_EUNSUPPORTED,
-              "als_topk: top %d at rank %d needs %zu B of LDS (> %d)", top, k, lds, kLdsBytes);
-  const unsigned grid = (unsigned)((n_q + 63) / 64);
+  const int rg = topk_split_rg(k, top);
+  if (rg == 0) {
+    const size_t lds = topk_lds_bytes(cn, top);
+    ALS_REQUIRE(lds <= kLdsBytes, ALS_EUNSUPPORTED,
+                "als_topk: top %d at rank %d needs %zu B of LDS (> %d)", top, k, lds, kLdsBytes);
+    const unsigned grid = (unsigned)((n_q + 63) / 64);
 #define ALS_TOPK_LAUNCH(CN)                                                                   \
   do {                                                                                        \
     ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_kernel<CN>),              \
@@ -235,11 +455,59 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     topk_kernel<CN><<<grid, 256, lds, st>>>(Q, n_q, V, n_v, ld, k, top, idx_out, score_out);  \
     ALS_LAUNCH_CHECK();                                                                       \
   } while (0)
-  if (cn == 1) ALS_TOPK_LAUNCH(1);
-  else if (cn == 2) ALS_TOPK_LAUNCH(2);
-  else if (cn == 4) ALS_TOPK_LAUNCH(4);
-  else ALS_TOPK_LAUNCH(8);
+    if (cn == 1) ALS_TOPK_LAUNCH(1);
+    else if (cn == 2) ALS_TOPK_LAUNCH(2);
+    else if (cn == 4) ALS_TOPK_LAUNCH(4);
+    else ALS_TOPK_LAUNCH(8);
 #undef ALS_TOPK_LAUNCH
+    return ALS_OK;
+  }
+  ALS_REQUIRE(ws != nullptr && ws_bytes >= als_topk_workspace_bytes(n_q, n_v, k, top),
+              ALS_EWORKSPACE, "als_topk: workspace %zu < %zu", ws_bytes,
+              als_topk_workspace_bytes(n_q, n_v, k, top));
+  ALS_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, ALS_EINVAL,
+              "als_topk: workspace must be 16-byte aligned");
+  unsigned* scal_u = static_cast<unsigned*>(ws);
+  const float* scal = reinterpret_cast<const float*>(scal_u);
+  _Float16* vsp = reinterpret_cast<_Float16*>(static_cast<char*>(ws) + 256);
+  const int kq = topk_kq(k);
+  const int kq_shift = __builtin_ctz(kq);
+  ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
+  const int64_t nq_el = n_q * (int64_t)ld, nv_el = n_v * (int64_t)ld;
+  tk_absmax_kernel<<<(int)std::min<int64_t>(1024, (nq_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
+      Q, nq_el, scal_u);
+  ALS_LAUNCH_CHECK();
+  if (n_v > 0) {
+    tk_absmax_kernel<<<(int)std::min<int64_t>(1024, (nv_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
+        V, nv_el, scal_u + 1);
+    ALS_LAUNCH_CHECK();
+    const int64_t total = n_v << kq_shift;
+    topk_split_table_kernel<<<(int)std::min<int64_t>(4096, (total + 255) / 256), 256, 0, st>>>(
+        V, n_v, ld, k, kq_shift, scal, vsp);
+    ALS_LAUNCH_CHECK();
+  }
+  const size_t lds = topk_split_lds_bytes(kq, rg, top);
+  const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
+  const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
+#define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                                                           \
+  do {                                                                                          \
+    ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG>),      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
+    topk_split_kernel<NK, RG><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, scal,      \
+                                                      idx_out, score_out);                      \
+    ALS_LAUNCH_CHECK();                                                                         \
+  } while (0)
+  if (kq == 32) {
+    if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);
+    else ALS_TOPK_SPLIT_LAUNCH(1, 1);
+  } else if (kq == 64) {
+    if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(2, 2);
+    else ALS_TOPK_SPLIT_LAUNCH(2, 1);
+  } else {
+    if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(4, 2);
+    else ALS_TOPK_SPLIT_LAUNCH(4, 1);
+  }
+#undef ALS_TOPK_SPLIT_LAUNCH
   return ALS_OK;
 }
 

@@ -210,8 +210,10 @@ def topk_rows(Q: torch.Tensor, n_q: int, V: torch.Tensor, n_v: int, rank: int, t
     L = _lib.lib()
     idx = torch.empty((n_q, top), dtype=torch.int32, device=Q.device)
     sc = torch.empty((n_q, top), dtype=torch.float32, device=Q.device)
-    check(L.als_topk(ptr(Q), n_q, ptr(V), n_v, Q.shape[1], rank, top, ptr(idx), ptr(sc), 0, 0,
-                     stream_ptr(Q.device)), "als_topk")
+    w = torch.empty(int(L.als_topk_workspace_bytes(n_q, n_v, rank, top)), dtype=torch.uint8,
+                    device=Q.device)
+    check(L.als_topk(ptr(Q), n_q, ptr(V), n_v, Q.shape[1], rank, top, ptr(idx), ptr(sc), ptr(w),
+                     w.numel(), stream_ptr(Q.device)), "als_topk")
     return idx, sc
 
 

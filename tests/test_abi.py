@@ -59,6 +59,8 @@ def test_workspace_sizes_are_monotone_and_host_only():
     assert L.als_yty_workspace_bytes(10 ** 6, 64) < L.als_yty_workspace_bytes(10 ** 6, 128)
     assert L.als_yty_workspace_bytes(10 ** 6, 64) > 0
     assert L.als_rmse_workspace_bytes(10 ** 6) > L.als_rmse_workspace_bytes(10)
+    assert L.als_topk_workspace_bytes(10, 1000, 64, 10) < L.als_topk_workspace_bytes(10, 10 ** 5, 64, 10)
+    assert L.als_topk_workspace_bytes(10, 1000, 32, 10) < L.als_topk_workspace_bytes(10, 1000, 128, 10)
     assert [L.als_k_pad(k) for k in (1, 16, 17, 32, 33, 64, 65, 128)] == [16, 16, 32, 32, 64, 64,
                                                                          128, 128]
 
@@ -98,6 +100,8 @@ def test_zero_size_calls_are_noops():
     L = _lib.lib()
     assert L.als_predict(0, 0, 0, 0, 0, 0, 0, 0, 0, 4, 4, 0, 0) == 0
     assert L.als_topk(0, 0, 0, 0, 4, 4, 1, 0, 0, 0, 0, 0) == 0
+    assert L.als_topk(1, 1, 1, 1, 64, 64, 10, 1, 1, 0, 0, 0) == -2      # split path needs ws
+    assert L.als_topk(1, 1, 1, 1, 64, 64, 10, 1, 1, 8, 1 << 20, 0) == -1  # ws not 16-B aligned
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")

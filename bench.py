@@ -142,7 +142,7 @@ def run_single(args):
         # Spark order: items from users, then users from items (ALS.train loop);
         # implicit: YtY of the source side before each half-sweep (computeYtY)
         yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
-        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 4)
+        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 12)
         if evs is not None:
             evs[0].record()
         E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
@@ -150,7 +150,7 @@ def run_single(args):
             evs[1].record()
         E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 2)
         yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
-        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 4)
+        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 12)
         if evs is not None:
             evs[2].record()
         E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
@@ -261,7 +261,7 @@ def run_distributed(args):
     dist.init_process_group("nccl", device_id=dev)
     rank, world = dist.get_rank(), dist.get_world_size()
     u, i, r = D.synthetic_config(args.config, device=dev, shard=rank)
-    sh = ShardedALS(u, i, r, device=dev)
+    sh = ShardedALS(u, i, r, device=dev, chunks=args.chunks)
     del u, i, r
     k = args.rank
     sh.init_factors(k, seed=5)
@@ -317,6 +317,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rmse", dest="rmse", action="store_false")
+    ap.add_argument("--chunks", type=int, default=None,
+                    help="row chunks per rank for the overlapped all-gathers (default 4 at N>1)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the sharded (RCCL) code path even with one rank")
     args = ap.parse_args()

@@ -108,11 +108,14 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * fp64 k_pad x k_pad Gram from als_yty.  status_dev: device int32, set to
  * (row+1) of a row whose Cholesky pivot was not positive (0 = all rows ok;
  * Spark raises from dppsv in that case).  ws: 16-byte aligned.
- * phases: bit 2 = prep (scale words; explicit: the split table of Y_src),
- * bit 0 = launch 1 (heavy-row chunk partials + fused light-row gram/solve),
- * bit 1 = launch 2 (heavy-row reduce + solve); 7 = all (the normal call).  They
- * run in the order prep, 1, 2; split across calls, issue them in that order on
- * one stream with the same workspace. */
+ * phases: bit 2 = Y_src prep (max |Y_src|; explicit: the split table), bit 3 =
+ * rating scale (max |rating| of this block), bit 0 = launch 1 (heavy-row chunk
+ * partials + fused light-row gram/solve), bit 1 = launch 2 (heavy-row reduce +
+ * solve); 15 = all (the normal call).  They run in the order 2, 3, 0, 1; split
+ * across calls, issue them in that order on one stream with the same
+ * workspace.  Blocks that share Y_src (row chunks of one half-sweep) may share
+ * one bit-2 prep: it sits at a fixed workspace offset (size the workspace for
+ * the largest n_chunks). */
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src);
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light,

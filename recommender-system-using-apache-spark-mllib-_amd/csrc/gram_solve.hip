@@ -1189,8 +1189,13 @@ __global__ __launch_bounds__(256) void absmax_csr_kernel(const int64_t* __restri
                                                          unsigned* __restrict__ out) {
   const int64_t n = row_ptr[n_rows];
   float m = 0.f;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-    m = fmaxf(m, fabsf(val[i]));
+  const int64_t n4 = n >> 2;  // val is 16-byte aligned (a CSR value array)
+  const float4* v4 = reinterpret_cast<const float4*>(val);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 v = v4[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = fmaxf(m, fabsf(val[4 * n4 + threadIdx.x]));
   block_absmax_publish(m, out);
 }
 
@@ -1630,15 +1635,16 @@ static size_t slot_doubles(int k) {
 
 extern "C" {
 
-static size_t solve_slots_bytes(int32_t k, int32_t n_chunks) {
-  return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
+static size_t solve_table_bytes(int32_t k, int64_t n_src) {
+  return align_up(sizeof(uint32_t) * (size_t)als_k_pad(k) * (size_t)((n_src > 0 ? n_src : 0) + 1));
 }
 
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src) {
-  // partial slots of the heavy-row chunks | 256 B of scale words | split table
-  // ((n_src + 1) x k_pad words, explicit feedback)
-  return solve_slots_bytes(k, n_chunks) + 256 +
-         align_up(sizeof(uint32_t) * (size_t)als_k_pad(k) * (size_t)((n_src > 0 ? n_src : 0) + 1));
+  // 256 B of scale words | split table ((n_src + 1) x k_pad words, explicit) |
+  // partial slots of the heavy-row chunks.  The first two sit at fixed offsets,
+  // so calls over blocks that share Y_src can share one prep (phases).
+  return 256 + solve_table_bytes(k, n_src) +
+         align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -1659,42 +1665,50 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   ALS_REQUIRE(reg >= 0.f && alpha >= 0.f, ALS_EINVAL, "als_solve_half: reg/alpha must be >= 0");
   ALS_REQUIRE((reinterpret_cast<uintptr_t>(Y_src) & 15) == 0, ALS_EINVAL,
               "als_solve_half: Y_src must be 16-byte aligned");
+  ALS_REQUIRE((reinterpret_cast<uintptr_t>(val) & 15) == 0, ALS_EINVAL,
+              "als_solve_half: val must be 16-byte aligned");
   ALS_REQUIRE(n_src >= 0 && n_src < (int64_t(1) << 31), ALS_EINVAL,
               "als_solve_half: n_src %lld not in [0, 2^31)", (long long)n_src);
   ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks, n_src), ALS_EWORKSPACE,
               "als_solve_half: workspace %zu < %zu", ws_bytes,
               als_solve_workspace_bytes(k, n_chunks, n_src));
-  ALS_REQUIRE(phases >= 1 && phases <= 7, ALS_EINVAL, "als_solve_half: phases must be in [1, 7]");
+  ALS_REQUIRE(phases >= 1 && phases <= 15, ALS_EINVAL,
+              "als_solve_half: phases must be in [1, 15]");
   ALS_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, ALS_EINVAL,
               "als_solve_half: workspace must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
-  double* slots = static_cast<double*>(ws);
-  // scale words (max |Y_src|, max |rating|), then the split table
-  unsigned* scal_u =
-      reinterpret_cast<unsigned*>(static_cast<char*>(ws) + solve_slots_bytes(k, n_chunks));
+  // scale words (max |Y_src|, max |rating|), the split table, the partial slots
+  unsigned* scal_u = static_cast<unsigned*>(ws);
   const float* scal = reinterpret_cast<const float*>(scal_u);
-  uint32_t* Ysp = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(scal_u) + 256);
+  uint32_t* Ysp = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256);
+  double* slots =
+      reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + solve_table_bytes(k, n_src));
   const int cn = cn_for_k(k);
   const int kp = als_k_pad(k);
   const int zero_row = (int)n_src;
-  if ((phases & 4) && n_chunks + n_light > 0) {
-    ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
-    ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
+  if (phases & 4) {  // Y_src prep: max |Y_src|, split table (explicit)
+    ALS_HIP(hipMemsetAsync(scal_u, 0, sizeof(unsigned), st));
     const int64_t ny = n_src * (int64_t)ld;
     if (ny > 0) {
       const int gy = (int)std::min<int64_t>(1024, (ny / 4 + 255) / 256 + 1);
       absmax_kernel<<<gy, 256, 0, st>>>(Y_src, ny, scal_u);
       ALS_LAUNCH_CHECK();
     }
-    // every row is light or heavy: the block's ratings are val[0, row_ptr[n_light + n_heavy])
-    absmax_csr_kernel<<<1024, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
-    ALS_LAUNCH_CHECK();
     if (!implicit) {
       const int kp4_shift = __builtin_ctz(kp / 4);
       const int64_t total = (n_src + 1) << kp4_shift;
       const int gt = (int)std::min<int64_t>(4096, (total + 255) / 256);
       split_table_kernel<<<gt, 256, 0, st>>>(Y_src, n_src, ld, k, kp4_shift, scal,
                                              reinterpret_cast<uint4*>(Ysp));
+      ALS_LAUNCH_CHECK();
+    }
+  }
+  if (phases & 8) {  // rating scale of this block: max |rating|
+    ALS_HIP(hipMemsetAsync(scal_u + 1, 0, sizeof(unsigned), st));
+    if (n_light + n_heavy > 0) {
+      ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
+      // every row is light or heavy: the block's ratings are val[0, row_ptr[n_light + n_heavy])
+      absmax_csr_kernel<<<1024, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
       ALS_LAUNCH_CHECK();
     }
   }

@@ -164,12 +164,14 @@ def compute_yty(Y: torch.Tensor, n: int, rank: int, ws: Workspace) -> torch.Tens
 
 def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, reg: float,
                implicit: bool, alpha: float, yty: Optional[torch.Tensor],
-               status: torch.Tensor, ws: Workspace, phases: int = 7) -> None:
+               status: torch.Tensor, ws: Workspace, phases: int = 15,
+               ws_chunks: Optional[int] = None) -> None:
     """One computeFactors pass: X[row] <- solve(A_row, b_row) for every row of `block`.
-    phases (bits, see als_hip.h): 4 = prep (scales, split table of Y), 1 = launch 1,
-    2 = launch 2; 7 = all three in order."""
+    phases (bits, see als_hip.h): 4 = Y prep (max |Y|, split table), 8 = rating scale,
+    1 = launch 1, 2 = launch 2; 15 = all in order.  ws_chunks: size the workspace for
+    this many heavy-row chunks (>= block.n_chunks; blocks sharing one Y prep)."""
     L = _lib.lib()
-    w = ws.get(L.als_solve_workspace_bytes(rank, block.n_chunks, Y.shape[0]))
+    w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0]))
     check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
                            ptr(block.light_rows), block.n_light, ptr(block.heavy_rows),
                            ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),

@@ -37,7 +37,7 @@ class OracleKernels:
     def yty(self, Y, n, rank):
         return torch.as_tensor(self.O.yty(Y[:n, :rank].numpy()))
 
-    def solve_half(self, block, Y, X, rank, reg, implicit, alpha, yty, status):
+    def solve_half(self, block, Y, X, rank, reg, implicit, alpha, yty, status, first=True):
         ptr, idx, val = block
         n = len(ptr) - 1
         if n == 0:
@@ -58,7 +58,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, implicit, out_dir):
+def _worker(rank, world, port, implicit, chunks, out_dir):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -74,7 +74,7 @@ def _worker(rank, world, port, implicit, out_dir):
         r = (r - 2.5).astype(np.float32)
     # arbitrary (non-aligned) input sharding: interleaved ratings
     sel = np.arange(len(u)) % world == rank
-    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
+    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=chunks)
     from oracle import als_oracle as O
     n_users = len(np.unique(u))
     U0 = O.initialize(n_users, 6, seed=2)
@@ -82,19 +82,20 @@ def _worker(rank, world, port, implicit, out_dir):
     uid, Uf = K.user_factors()
     iid, Vf = K.item_factors()
     if rank == 0:
-        np.savez(os.path.join(out_dir, f"dist_{int(implicit)}.npz"), uid=uid.numpy(),
+        np.savez(os.path.join(out_dir, f"dist_{int(implicit)}_{chunks}.npz"), uid=uid.numpy(),
                  U=Uf.numpy(), iid=iid.numpy(), V=Vf.numpy(), nnz=K.nnz,
                  u_starts=K.users.starts.numpy(), i_starts=K.items.starts.numpy(),
                  local=[K.user_rows, K.item_rows])
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("implicit", [False, True])
-def test_sharded_als_matches_single_process(tmp_path, implicit):
+@pytest.mark.parametrize("implicit,chunks", [(False, None), (True, None), (False, 3), (True, 3)])
+def test_sharded_als_matches_single_process(tmp_path, implicit, chunks):
+    """chunks=3: the [C, world, rows] layout with async per-chunk all-gathers."""
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), implicit, str(tmp_path)), nprocs=world,
+    mp.spawn(_worker, args=(world, _free_port(), implicit, chunks, str(tmp_path)), nprocs=world,
              join=True)
-    d = np.load(tmp_path / f"dist_{int(implicit)}.npz")
+    d = np.load(tmp_path / f"dist_{int(implicit)}_{chunks}.npz")
     from oracle import als_oracle as O
     u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
     if implicit:

@@ -22,8 +22,8 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize("implicit", [False, True])
-def test_sharded_one_rank_matches_engine(implicit):
+@pytest.mark.parametrize("implicit,chunks", [(False, None), (True, None), (False, 3)])
+def test_sharded_one_rank_matches_engine(implicit, chunks):
     import als_mi355x.engine as E
     from als_mi355x.distributed import ShardedALS
     u, i, r = planted(400, 300, density=0.05, seed=7, heavy_items=(1,))
@@ -37,7 +37,8 @@ def test_sharded_one_rank_matches_engine(implicit):
         core.init_factors(16, seed=3)
         U0 = core.U[:, :16].cpu().numpy()
         core.fit(16, 3, 0.1, implicit=implicit, alpha=3.0, U0=U0)
-        sh = ShardedALS(u, i, r, device="cuda:0")
+        # chunks=3: the chunked [C, world, rows] layout with async per-chunk all-gathers
+        sh = ShardedALS(u, i, r, device="cuda:0", chunks=chunks)
         sh.fit(16, 3, 0.1, implicit=implicit, alpha=3.0, U0_global=U0)
         _, Us = sh.user_factors()
         _, Vs = sh.item_factors()

@@ -110,6 +110,34 @@ def test_half_sweep_parity(rank, implicit):
     assert eu <= 1e-4
 
 
+@pytest.mark.parametrize("rscale,yscale,rank", [(1e3, 1.0, 16), (1e-3, 1.0, 16), (1.0, 1e4, 16),
+                                                (1.0, 1e-4, 64), (0.0, 1.0, 16), (-1.0, 1.0, 100)])
+def test_half_sweep_scale_extremes(rscale, yscale, rank):
+    """The split-f16 Gram scales its operands by powers of two from max|Y| and max|r|
+    (computed on the device per call): parity must hold far from unit magnitudes, for
+    negative ratings and for all-zero ratings (x = 0)."""
+    u, i, r = planted(400, 300, density=0.05, heavy_items=(3,), seed=17)
+    r = (r * rscale).astype(np.float32)
+    core = _core(u, i, r, chunk=128)
+    core.init_factors(rank, seed=3)
+    core.U.mul_(yscale)
+    U0 = core.U[:, :rank].cpu().numpy()
+    reg = 0.1 * yscale * yscale  # same conditioning as at unit scale
+    core.half_sweep_items(reg, False, 1.0)
+    torch.cuda.synchronize()
+    assert int(core.status.item()) == 0
+    ib = core.item_block
+    V = core.V[:, :rank].cpu().numpy()
+    V_ref = O.half_sweep(ib.row_ptr.cpu().numpy(), ib.col.cpu().numpy(), ib.val.cpu().numpy(),
+                         U0, reg, False, 1.0)
+    if rscale == 0.0:
+        assert np.all(V == 0.0) and np.all(V_ref == 0.0)
+        return
+    ev = rel_row_err(V, V_ref)
+    report(f"half_sweep_scale[r*{rscale},y*{yscale},rank={rank}]", ev)
+    assert ev <= 1e-4
+
+
 @pytest.mark.parametrize("rank", [3, 16, 40, 64, 100, 128])
 def test_yty_parity(rank):
     rng = np.random.default_rng(rank)

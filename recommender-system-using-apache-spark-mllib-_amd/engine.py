@@ -251,6 +251,42 @@ class ALSCore:
         self.V: Optional[torch.Tensor] = None
         self.rank = 0
 
+    @classmethod
+    def from_factors(cls, user_ids, U, item_ids, V, device=None) -> "ALSCore":
+        """A serving-only core (no ratings, cannot fit) from saved factors: ids ascending,
+        U/V host or device arrays [n, rank].  predict / rmse / top-k run as after fit()."""
+        _lib.require_gpu()
+        self = cls.__new__(cls)
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.ws = Workspace(self.device)
+        self.nnz = 0
+        self.user_block = self.item_block = None
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        U = _to_device(U, torch.float32, self.device)
+        V = _to_device(V, torch.float32, self.device)
+        rank = int(U.shape[1])
+        if V.shape[1] != rank or not (1 <= rank <= MAX_RANK):
+            raise ValueError(f"factor ranks {U.shape[1]}/{V.shape[1]} invalid (max {MAX_RANK})")
+        idx = []
+        for ids, F in ((user_ids, U), (item_ids, V)):
+            ids = _to_device(ids, torch.int32, self.device)
+            if ids.numel() != F.shape[0] or ids.numel() == 0 or int(ids.min()) < 0:
+                raise ValueError("factor ids must be non-empty, non-negative and match the rows")
+            if ids.numel() > 1 and not bool((ids[1:] > ids[:-1]).all()):
+                raise ValueError("factor ids must be strictly ascending")
+            mp = torch.full((int(ids.max()) + 1,), -1, dtype=torch.int32, device=self.device)
+            mp[ids.long()] = torch.arange(ids.numel(), dtype=torch.int32, device=self.device)
+            idx.append(IdIndex(mp, ids.clone(), int(ids.numel())))
+        self.uidx, self.iidx = idx
+        self.rank = rank
+        ld = ld_for(rank)
+        self.U = torch.zeros((U.shape[0], ld), dtype=torch.float32, device=self.device)
+        self.V = torch.zeros((V.shape[0], ld), dtype=torch.float32, device=self.device)
+        self.U[:, :rank] = U
+        self.V[:, :rank] = V
+        return self
+
     @property
     def n_users(self) -> int:
         return self.uidx.n

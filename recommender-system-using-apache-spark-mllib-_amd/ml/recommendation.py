@@ -169,6 +169,25 @@ class ALSModel:
         F = F.float().cpu().numpy()
         return pd.DataFrame({"id": ids, "features": list(F)})
 
+    def save(self, path: str, overwrite: bool = False) -> None:
+        """ALSModel.save(path) / write().save(path) in Spark's layout."""
+        from .. import persistence
+        uids, U = self._core.user_factors()
+        iids, V = self._core.item_factors()
+        params = {k: v for k, v in self._p.items() if isinstance(v, (int, float, str, bool))}
+        persistence.save_ml(path, "ALSModel_mi355x", params, self.rank, uids.cpu().numpy(),
+                            U.cpu().numpy(), iids.cpu().numpy(), V.cpu().numpy(),
+                            overwrite=overwrite)
+
+    @classmethod
+    def load(cls, path: str) -> "ALSModel":
+        """ALSModel.load(path): factors back into HBM (serving only), params restored."""
+        from .. import persistence
+        _, params, _, uids, U, iids, V = persistence.load_ml(path)
+        p = dict(_Params._defaults)
+        p.update({k: v for k, v in params.items() if k in p})
+        return cls(_engine.ALSCore.from_factors(uids, U, iids, V), p)
+
     @property
     def userFactors(self):
         return self._factors_df(*self._core.user_factors())

@@ -142,6 +142,22 @@ class MatrixFactorizationModel:
         return [(int(k), [Rating(int(k), int(a), float(s)) for a, s in zip(ri, rs) if a >= 0])
                 for k, ri, rs in zip(keys, ids, sc)]
 
+    def save(self, sc, path: str, overwrite: bool = False) -> None:
+        """MatrixFactorizationModel.save(sc, path) in Spark's layout (``sc`` is ignored)."""
+        from .. import persistence
+        uids, U = self._core.user_factors()
+        pids, V = self._core.item_factors()
+        persistence.save_mllib(path, self.rank, uids.cpu().numpy(), U.cpu().numpy(),
+                               pids.cpu().numpy(), V.cpu().numpy(), overwrite=overwrite)
+
+    @classmethod
+    def load(cls, sc, path: str) -> "MatrixFactorizationModel":
+        """MatrixFactorizationModel.load(sc, path): factors back into HBM (serving only)."""
+        from .. import persistence
+        _, uids, U, pids, V = persistence.load_mllib(path)
+        return cls(_engine.ALSCore.from_factors(uids, U.astype(np.float32), pids,
+                                                V.astype(np.float32)))
+
     def recommendUsersForProducts(self, num: int):
         ids, sc = self._core.recommend_items(int(num))
         keys = self._core.iidx.uniq.cpu().numpy()

@@ -1315,12 +1315,15 @@ __device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], floa
     __syncthreads();
     // (b) panel: lanes 0..15 diagonal block, lanes 16.. tiles K+1+3R ..
     constexpr int NOFF = NB - 1 - K;  // off-diagonal tiles in block row K
+    // Every active wave factors the diagonal block B_KK redundantly from its slot,
+    // so wave 0 must not overwrite that slot (nor the diagonal rhs RB[16K..]) until
+    // all waves have read it: its U_KK columns stay in R16 until after the barrier.
+    float R16[16];
     if constexpr (R == 0 || 3 * R < NOFF) {
       const int Jl0 = q == 0 ? K : K + 3 * R + q;
       const bool col_ok = Jl0 < NB;
       const int Jl = col_ok ? Jl0 : K;
       float* colp = slot(K, Jl) + m * CS;
-      float R16[16];
 #pragma unroll
       for (int c2 = 0; c2 < 8; ++c2) {
         const float2 v = *reinterpret_cast<const float2*>(colp + 2 * c2);
@@ -1342,7 +1345,7 @@ __device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], floa
         myd = put_lane<p>(myd, d);
       });
       okl = okl && (myd > 0.f);  // lanes >= 16 keep myd = 1; NaN pivots fail
-      if (col_ok && (q > 0 || R == 0)) {
+      if (col_ok && q > 0) {
 #pragma unroll
         for (int c2 = 0; c2 < 8; ++c2)
           *reinterpret_cast<float2*>(colp + 2 * c2) = make_float2(R16[2 * c2], R16[2 * c2 + 1]);
@@ -1354,6 +1357,16 @@ __device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], floa
       }
     }
     __syncthreads();
+    if constexpr (R == 0) {
+      // U_KK columns -> the diagonal slot, now that no wave reads B_KK any more
+      // (read again only by this wave's back substitution)
+      if (lane < 16) {
+        float* colp = slot(K, K) + m * CS;
+#pragma unroll
+        for (int c2 = 0; c2 < 8; ++c2)
+          *reinterpret_cast<float2*>(colp + 2 * c2) = make_float2(R16[2 * c2], R16[2 * c2 + 1]);
+      }
+    }
     // (c) trailing update of this wave's tiles: B_IJ -= (D_K U_KI)^T U_KJ
     if constexpr (K + 1 < NB) {
       float dq[4];

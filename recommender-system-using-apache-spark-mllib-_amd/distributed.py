@@ -9,7 +9,11 @@ data-movement site" table, §8e):
     half (factors are replicated; each rank solves only its own rows), issued
     per row chunk and overlapped with the solve of the next chunk;
   * computeYtY's treeAggregate (implicit)    -> local YtY of the rank's own rows +
-    all_reduce of the k_pad^2 fp64 Gram.
+    all_reduce of the k_pad^2 fp64 Gram;
+  * computeError's reduce + count (RecommenderSystem.py:123, :126)
+                                             -> local fused (sse, n) + all_reduce;
+  * predict / recommendForAll                -> local: the factors are replicated
+    after every half-sweep, so no collective (each rank scores its own users).
 
 Rows are split into contiguous, nnz-balanced ranges of the global dense index
 (no row is split across ranks), and each rank's range into C nnz-balanced
@@ -22,18 +26,24 @@ copy), and CSR column indices are stored in that padded numbering.  A
 half-sweep solves chunk c, then starts its all-gather (async, RCCL's stream)
 while chunk c+1 is solved; the waits come before the next half-sweep.
 
+The initial factors are drawn from the seed over the GLOBAL dense user rows
+(exactly ALSCore.init_factors' draw) and each rank keeps its slice, so a fit is
+independent of the world size.
+
 The arithmetic is delegated to a `kernels` object (default: the HIP kernels of
 libals_hip.so).  Tests substitute the CPU oracle to check the coordination
 logic with the gloo backend on CPU.
 """
 from __future__ import annotations
 
+import math
 from dataclasses import dataclass
 from typing import Optional
 
-import numpy as np
 import torch
 import torch.distributed as dist
+
+from .engine import id_offset
 
 
 class HipKernels:
@@ -71,14 +81,21 @@ class HipKernels:
         self.E.solve_half(block, Y, X, rank, reg, implicit, alpha, yty, status, self.ws,
                           phases=15 if first else 11, ws_chunks=self.max_chunks)
 
+    def predict(self, u_keys, i_keys, umap, imap, U, V, rank) -> torch.Tensor:
+        E = self.E
+        return E.predict_pairs(u_keys, i_keys, E.IdIndex(umap, umap, 0), E.IdIndex(imap, imap, 0),
+                               U, V, rank)
+
+    def rmse_partial(self, u_keys, i_keys, r, umap, imap, U, V, rank) -> torch.Tensor:
+        E = self.E
+        return E.rmse_pairs(u_keys, i_keys, r, E.IdIndex(umap, umap, 0),
+                            E.IdIndex(imap, imap, 0), U, V, rank, self.ws)
+
+    def topk(self, Q, n_q, V, n_v, rank, top):
+        return self.E.topk_rows(Q, n_q, V, n_v, rank, top)
+
     def ld(self, rank: int) -> int:
         return self.E.ld_for(rank)
-
-
-def _all_gather_cat(t: torch.Tensor, world: int, group) -> torch.Tensor:
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t, group=group)
-    return torch.cat(out)
 
 
 def _ranges(deg: torch.Tensor, world: int):
@@ -101,8 +118,10 @@ class SideLayout:
     starts: torch.Tensor   # [world+1] dense row ranges of the ranks (cpu int64)
     cstarts: torch.Tensor  # [world, C+1] dense row ranges of each rank's chunks (cpu int64)
     rows_per_chunk: int    # padded rows per (chunk, rank)
-    dense_map: torch.Tensor  # id -> dense row (-1 absent), device int32
-    uniq: torch.Tensor       # dense row -> id, device int32
+    dense_map: torch.Tensor  # (id - offset) -> dense row (-1 absent), device int32
+    uniq: torch.Tensor       # dense row -> id - offset, device int32
+    offset: int = 0          # ids are keyed as id - offset (engine.id_offset)
+    _pmap: Optional[torch.Tensor] = None
 
     @property
     def chunks(self) -> int:
@@ -111,6 +130,14 @@ class SideLayout:
     @property
     def rows_per_rank(self) -> int:
         return self.chunks * self.rows_per_chunk
+
+    def ids(self) -> torch.Tensor:
+        return self.uniq if self.offset == 0 else (self.uniq.long() + self.offset).to(torch.int32)
+
+    def keys(self, ids: torch.Tensor) -> torch.Tensor:
+        """ids -> map keys (-1 outside the mapped range)."""
+        s = ids.long() - self.offset
+        return torch.where((s >= 0) & (s < self.dense_map.numel()), s, -1).to(torch.int32)
 
     def owner_of(self, dense: torch.Tensor) -> torch.Tensor:
         st = self.starts.to(dense.device)
@@ -124,6 +151,16 @@ class SideLayout:
         o, c = g // C, g % C
         return ((c * W + o) * self.rows_per_chunk + (dense.long() - b[g])).to(torch.int32)
 
+    def padded_map(self) -> torch.Tensor:
+        """(id - offset) -> padded row (-1 absent): the id map of the replicated tables."""
+        if self._pmap is None:
+            d = self.dense_map
+            pm = torch.full_like(d, -1)
+            ok = d >= 0
+            pm[ok] = self.padded(d[ok])
+            self._pmap = pm
+        return self._pmap
+
     def chunk_rows(self, rank: int, c: int) -> int:
         return int(self.cstarts[rank, c + 1] - self.cstarts[rank, c])
 
@@ -134,7 +171,7 @@ class ShardedALS:
     def __init__(self, users, items, ratings, device=None, group=None, kernels=None,
                  chunks: Optional[int] = None):
         self.group = group
-        self.rank = dist.get_rank(group)
+        self.proc = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         # row chunks per rank: the all-gather of chunk c overlaps the solve of c+1.
         # Each chunk is its own launch (its own tail): measured +0.15 ms per
@@ -151,13 +188,23 @@ class ShardedALS:
         i = torch.as_tensor(items).to(dev, torch.int32)
         r = torch.as_tensor(ratings).to(dev, torch.float32)
         self.local_nnz = int(u.numel())
-        mx = torch.tensor([int(u.max()) if u.numel() else -1, int(i.max()) if i.numel() else -1],
-                          dtype=torch.int64, device=dev)
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX, group=group)
-        u_space, i_space = int(mx[0]) + 1, int(mx[1]) + 1
+        big = 1 << 40
+        mm = torch.tensor([int(u.max()) if u.numel() else -big, int(i.max()) if i.numel() else -big,
+                           -int(u.min()) if u.numel() else -big,
+                           -int(i.min()) if i.numel() else -big], dtype=torch.int64, device=dev)
+        dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
+        (umax, imax), (umin, imin) = mm[:2].tolist(), (-mm[2:]).tolist()
+        if umax < umin:
+            raise ValueError("ALS needs at least one rating")
+        uoff, ioff = id_offset(umin, umax), id_offset(imin, imax)
+        u_space, i_space = umax - uoff + 1, imax - ioff + 1
+        if uoff:
+            u = (u.long() - uoff).to(torch.int32)
+        if ioff:
+            i = (i.long() - ioff).to(torch.int32)
         self.chunks = self._chunks_arg or self._auto_chunks(u_space, i_space)
-        self.users = self._layout(u, u_space)
-        self.items = self._layout(i, i_space)
+        self.users = self._layout(u, u_space, uoff)
+        self.items = self._layout(i, i_space, ioff)
         nz = torch.tensor([self.local_nnz], dtype=torch.int64, device=dev)
         dist.all_reduce(nz, group=group)
         self.nnz = int(nz)
@@ -173,7 +220,8 @@ class ShardedALS:
         self.item_rows = self._local_rows(self.items)
         self.item_blocks = self._blocks(self.items, ri_, rc_, rv_, self.users)
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.rank_k = 0
+        self.rank = 0  # factor rank (k); the process rank is self.proc
+        self._dense_cache = {}
 
     # ---- setup helpers ----
     def _auto_chunks(self, u_space: int, i_space: int) -> int:
@@ -183,12 +231,13 @@ class ShardedALS:
             return 1
         return 4 if max(u_space, i_space) // self.world >= (1 << 20) else 1
 
-    def _layout(self, ids: torch.Tensor, space: int) -> SideLayout:
+    def _layout(self, ids: torch.Tensor, space: int, offset: int) -> SideLayout:
         dev = self.device
         flag = torch.zeros(space, dtype=torch.int32, device=dev)
         flag[ids.long()] = 1
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
         present = torch.nonzero(flag).flatten().to(torch.int32)
+        del flag
         dmap, uniq, n = self.K.index_build(present, space)
         deg = torch.zeros(n, dtype=torch.int64, device=dev)
         deg.index_add_(0, dmap[ids.long()].long(), torch.ones_like(ids, dtype=torch.int64))
@@ -198,10 +247,10 @@ class ShardedALS:
         cst = torch.stack([_ranges(degc[int(starts[w]):int(starts[w + 1])], self.chunks)
                            + starts[w] for w in range(self.world)])
         rpc = max(int((cst[:, 1:] - cst[:, :-1]).max()), 1)
-        return SideLayout(n, starts, cst, rpc, dmap, uniq)
+        return SideLayout(n, starts, cst, rpc, dmap, uniq, offset)
 
     def _local_rows(self, side: SideLayout) -> int:
-        return int(side.starts[self.rank + 1] - side.starts[self.rank])
+        return int(side.starts[self.proc + 1] - side.starts[self.proc])
 
     def _blocks(self, side: SideLayout, rows_pad, cols_pad, vals, other: SideLayout):
         """Per-chunk rating blocks of this rank's rows (rows_pad: padded positions)."""
@@ -211,7 +260,7 @@ class ShardedALS:
         j = (p % rpc).to(torch.int32)
         out = []
         for cc in range(side.chunks):
-            n_c = side.chunk_rows(self.rank, cc)
+            n_c = side.chunk_rows(self.proc, cc)
             sel = c == cc
             out.append(self.K.build_block(j[sel], cols_pad[sel], vals[sel], n_c,
                                           W * other.rows_per_rank) if n_c > 0 else None)
@@ -231,10 +280,22 @@ class ShardedALS:
             out.append(o)
         return out
 
+    @property
+    def n_users(self) -> int:
+        return self.users.n
+
+    @property
+    def n_items(self) -> int:
+        return self.items.n
+
     # ---- ALS ----
-    def init_factors(self, rank: int, seed: int = 0, U0_global: Optional[torch.Tensor] = None):
-        """U in the padded layout.  U0_global: optional [n_users_dense, rank] start."""
-        self.rank_k = rank
+    def init_factors(self, rank: int, seed: int = 0, U0=None, U0_global=None):
+        """U in the padded layout.  The default draw is ALSCore.init_factors' one over
+        all global dense user rows (unit-norm Gaussian rows from `seed`), sliced to
+        this rank's rows; U0 / U0_global: an explicit [n_users_dense, rank] start."""
+        U0 = U0 if U0 is not None else U0_global
+        self.rank = rank
+        self._dense_cache = {}
         ld = self.K.ld(rank)
         dev = self.device
         W = self.world
@@ -245,26 +306,27 @@ class ShardedALS:
                                  device=dev)
         self.V_loc = torch.zeros((its.chunks, its.rows_per_chunk, ld), dtype=torch.float32,
                                  device=dev)
-        cs = us.cstarts[self.rank]
+        cs = us.cstarts[self.proc]
         s0 = int(cs[0])
         n_loc = self.user_rows
-        if U0_global is not None:
-            x = torch.as_tensor(U0_global).to(dev, torch.float32)[s0:s0 + n_loc, :rank]
+        if U0 is not None:
+            x = torch.as_tensor(U0).to(dev, torch.float32)[s0:s0 + n_loc, :rank]
         else:
             g = torch.Generator(device=dev)
-            g.manual_seed((int(seed) * 1000003 + self.rank) & 0x7FFFFFFFFFFFFFFF)
-            x = torch.randn((n_loc, rank), generator=g, device=dev)
-            x = x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
+            g.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
+            x = torch.randn((us.n, rank), generator=g, device=dev, dtype=torch.float32)
+            x = (x / torch.linalg.vector_norm(x, dim=1, keepdim=True))[s0:s0 + n_loc]
         for c in range(us.chunks):
             a, b = int(cs[c]) - s0, int(cs[c + 1]) - s0
             self.U_loc[c, :b - a, :rank] = x[a:b]
+        del x
         full = self.U_full.view(us.chunks, -1, ld)
         for c in range(us.chunks):
             dist.all_gather_into_tensor(full[c], self.U_loc[c], group=self.group)
 
     def _yty(self, loc: torch.Tensor):
         # local rows of every chunk (padding rows are zero and add nothing), then all_reduce
-        g = self.K.yty(loc.view(-1, loc.shape[-1]), loc.shape[0] * loc.shape[1], self.rank_k)
+        g = self.K.yty(loc.view(-1, loc.shape[-1]), loc.shape[0] * loc.shape[1], self.rank)
         dist.all_reduce(g, group=self.group)
         return g
 
@@ -275,13 +337,14 @@ class ShardedALS:
         first = True
         for c, blk in enumerate(blocks):
             if blk is not None:
-                self.K.solve_half(blk, Y_full, X_loc[c], self.rank_k, reg, implicit, alpha, yty,
+                self.K.solve_half(blk, Y_full, X_loc[c], self.rank, reg, implicit, alpha, yty,
                                   self.status, first=first)
                 first = False
             works.append(dist.all_gather_into_tensor(Xf[c], X_loc[c], group=self.group,
                                                      async_op=True))
         for w in works:
             w.wait()
+        self._dense_cache = {}
 
     def half_sweep_items(self, reg, implicit=False, alpha=1.0):
         yty = self._yty(self.U_loc) if implicit else None
@@ -297,24 +360,105 @@ class ShardedALS:
         self.half_sweep_items(reg, implicit, alpha)
         self.half_sweep_users(reg, implicit, alpha)
 
-    def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0_global=None):
-        self.init_factors(rank, seed, U0_global)
-        self.status.zero_()
-        for _ in range(max_iter):
-            self.iterate(reg, implicit, alpha)
+    def check_status(self) -> None:
         st = self.status.clone()
         dist.all_reduce(st, op=dist.ReduceOp.MAX, group=self.group)
         if int(st) != 0:
-            raise RuntimeError("Cholesky failed (non-positive pivot) on some rank")
+            raise RuntimeError("Cholesky failed (non-positive pivot) on some rank: the normal "
+                               "equations are not positive definite (Spark raises from dppsv)")
+
+    def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0=None,
+            U0_global=None):
+        self.init_factors(rank, seed, U0, U0_global)
+        self.status.zero_()
+        for _ in range(max_iter):
+            self.iterate(reg, implicit, alpha)
+        self.check_status()
         return self
 
-    # ---- factor views in dense order (replicated on every rank) ----
-    def _dense_rows(self, side: SideLayout, full: torch.Tensor) -> torch.Tensor:
-        dense = torch.arange(side.n, device=full.device)
-        return full[side.padded(dense).long(), :self.rank_k]
+    # ---- serving protocol (engine.ALSCore's), on the replicated factors ----
+    def _dense(self, user_side: bool) -> torch.Tensor:
+        """Dense-order copy [n, ld] of one replicated factor table (cached per fit state)."""
+        if user_side not in self._dense_cache:
+            side, full = (self.users, self.U_full) if user_side else (self.items, self.V_full)
+            dense = torch.arange(side.n, device=full.device)
+            self._dense_cache[user_side] = full[side.padded(dense).long()].contiguous()
+        return self._dense_cache[user_side]
 
+    def _ids(self, x) -> torch.Tensor:
+        return torch.as_tensor(x).to(self.device).to(torch.int32)
+
+    def predict(self, users, items) -> torch.Tensor:
+        """fp64 <u, v> of this rank's pairs (NaN for unknown ids); no collective."""
+        us, its = self.users, self.items
+        return self.K.predict(us.keys(self._ids(users)), its.keys(self._ids(items)),
+                              us.padded_map(), its.padded_map(), self.U_full, self.V_full,
+                              self.rank)
+
+    def rmse(self, users, items, ratings):
+        """computeError over the pairs of ALL ranks: local fused (sse, n), then an
+        all_reduce (RecommenderSystem.py:123 reduce, :126 count)."""
+        us, its = self.users, self.items
+        r = torch.as_tensor(ratings).to(self.device, torch.float32)
+        part = self.K.rmse_partial(us.keys(self._ids(users)), its.keys(self._ids(items)), r,
+                                   us.padded_map(), its.padded_map(), self.U_full, self.V_full,
+                                   self.rank).to(torch.float64)
+        dist.all_reduce(part, group=self.group)
+        sse, n = part.tolist()
+        return (math.sqrt(sse / n) if n > 0 else float("nan")), int(n)
+
+    def recommend_all(self, top: int, user_side: bool = True):
+        """recommendForAll for THIS rank's rows of one side (its partition), against
+        the replicated other side: (keys, ids [m, t], scores [m, t]); no collective."""
+        side, loc = (self.users, self.U_loc) if user_side else (self.items, self.V_loc)
+        other = self.items if user_side else self.users
+        Vd = self._dense(not user_side)
+        t = min(int(top), other.n)
+        keys, ids, scs = [], [], []
+        cs = side.cstarts[self.proc]
+        oids = other.ids()
+        for c in range(side.chunks):
+            a, b = int(cs[c]), int(cs[c + 1])
+            if b <= a:
+                continue
+            idx, sc = self.K.topk(loc[c], b - a, Vd, other.n, self.rank, top)
+            keys.append(side.ids()[a:b])
+            ids.append(oids[idx[:, :t].long()])
+            scs.append(sc[:, :t])
+        if not keys:
+            e = torch.empty((0, t), device=self.device)
+            return torch.empty(0, dtype=torch.int32, device=self.device), e.int(), e
+        return torch.cat(keys), torch.cat(ids), torch.cat(scs)
+
+    def recommend_subset(self, ids, top: int, user_side: bool = True):
+        side = self.users if user_side else self.items
+        other = self.items if user_side else self.users
+        keys = torch.unique(self._ids(ids))
+        k = side.keys(keys)
+        rows = torch.full_like(k, -1, dtype=torch.long)
+        ok = k >= 0
+        rows[ok] = side.dense_map[k[ok].long()].long()
+        keys, rows = keys[rows >= 0], rows[rows >= 0]
+        t = min(int(top), other.n)
+        if keys.numel() == 0:
+            e = torch.empty((0, t), device=self.device)
+            return keys, e.int(), e
+        Q = self._dense(user_side).index_select(0, rows).contiguous()
+        idx, sc = self.K.topk(Q, keys.numel(), self._dense(not user_side), other.n, self.rank,
+                              top)
+        return keys, other.ids()[idx[:, :t].long()], sc[:, :t]
+
+    def recommend_users(self, top: int):
+        _, ids, sc = self.recommend_all(top, True)
+        return ids, sc
+
+    def recommend_items(self, top: int):
+        _, ids, sc = self.recommend_all(top, False)
+        return ids, sc
+
+    # ---- factor views in dense order (replicated on every rank) ----
     def user_factors(self):
-        return self.users.uniq, self._dense_rows(self.users, self.U_full)
+        return self.users.ids(), self._dense(True)[:, :self.rank]
 
     def item_factors(self):
-        return self.items.uniq, self._dense_rows(self.items, self.V_full)
+        return self.items.ids(), self._dense(False)[:, :self.rank]

@@ -59,14 +59,50 @@ def _to_device(x, dtype, device) -> torch.Tensor:
 # ---------------------------------------------------------------------------
 @dataclass
 class IdIndex:
-    """Dense id map of one side (the device form of Spark's sorted InBlock.srcIds)."""
-    map: torch.Tensor       # int32 [id_space]
-    uniq: torch.Tensor      # int32 [n]   ascending ids
+    """Dense id map of one side (the device form of Spark's sorted InBlock.srcIds).
+
+    Spark accepts any Int id (negative ones included).  The map is indexed by
+    `id - offset`; `offset` is the smallest id when ids are negative or the id
+    range starts far above 0, else 0 (ids used directly)."""
+    map: torch.Tensor       # int32 [id_space], (id - offset) -> dense row or -1
+    uniq: torch.Tensor      # int32 [n]   ascending ids - offset
     n: int
+    offset: int = 0
 
     @property
     def id_space(self) -> int:
         return int(self.map.numel())
+
+    def ids(self) -> torch.Tensor:
+        """The original ids of the dense rows (ascending), int32."""
+        return self.uniq if self.offset == 0 else (self.uniq.long() + self.offset).to(torch.int32)
+
+    def rows_of(self, ids: torch.Tensor) -> torch.Tensor:
+        """Dense row (int64) of each id, -1 when unknown."""
+        k = ids.long() - self.offset
+        ok = (k >= 0) & (k < self.id_space)
+        out = torch.full_like(k, -1)
+        out[ok] = self.map[k[ok]].long()
+        return out
+
+    def keys(self, ids: torch.Tensor) -> torch.Tensor:
+        """Query ids -> map keys; ids outside the mapped range -> -1 (unknown)."""
+        if self.offset == 0:
+            return ids.to(torch.int32).contiguous()
+        s = ids.long() - self.offset
+        return torch.where((s >= 0) & (s < self.id_space), s, -1).to(torch.int32).contiguous()
+
+
+MAX_ID_SPACE = 2 ** 31 - 1   # the map is indexed by int32
+
+
+def id_offset(lo: int, hi: int) -> int:
+    """Map offset for ids in [lo, hi]: 0 for the usual non-negative, compact ids."""
+    off = 0 if (lo >= 0 and hi < (1 << 26)) else lo
+    if hi - off + 1 > MAX_ID_SPACE:
+        raise ValueError(f"id range [{lo}, {hi}] spans more than 2^31-1 values; this build "
+                         "indexes ids through a dense int32 map")
+    return off
 
 
 def build_index(ids: torch.Tensor, id_space: int, ws: Workspace) -> IdIndex:
@@ -188,6 +224,7 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
 def predict_pairs(u: torch.Tensor, i: torch.Tensor, uidx: IdIndex, iidx: IdIndex,
                   U: torch.Tensor, V: torch.Tensor, rank: int) -> torch.Tensor:
     L = _lib.lib()
+    u, i = uidx.keys(u), iidx.keys(i)
     out = torch.empty(u.numel(), dtype=torch.float64, device=U.device)
     check(L.als_predict(ptr(u), ptr(i), u.numel(), ptr(uidx.map), uidx.id_space, ptr(iidx.map),
                         iidx.id_space, ptr(U), ptr(V), U.shape[1], rank, ptr(out),
@@ -198,6 +235,7 @@ def predict_pairs(u: torch.Tensor, i: torch.Tensor, uidx: IdIndex, iidx: IdIndex
 def rmse_pairs(u, i, r, uidx: IdIndex, iidx: IdIndex, U, V, rank: int, ws: Workspace):
     """(sse, count) over pairs with both ids known (computeError's join)."""
     L = _lib.lib()
+    u, i = uidx.keys(u), iidx.keys(i)
     out = torch.empty(2, dtype=torch.float64, device=U.device)
     w = ws.get(L.als_rmse_workspace_bytes(u.numel()))
     check(L.als_rmse_partial(ptr(u), ptr(i), ptr(r), u.numel(), ptr(uidx.map), uidx.id_space,
@@ -222,6 +260,18 @@ def topk_rows(Q: torch.Tensor, n_q: int, V: torch.Tensor, n_v: int, rank: int, t
 # ---------------------------------------------------------------------------
 # The engine
 # ---------------------------------------------------------------------------
+def make_engine(users, items, ratings, device=None):
+    """The engine behind ALS.fit / ALS.train: one GPU (ALSCore), or — when this process
+    is one rank of an initialised torch.distributed group of world size > 1 —
+    the sharded engine (distributed.ShardedALS), fed with this rank's partition
+    of the ratings (the role of a Spark DataFrame partition)."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        from .distributed import ShardedALS
+        return ShardedALS(users, items, ratings, device=device)
+    return ALSCore(users, items, ratings, device=device)
+
+
 class ALSCore:
     """Ratings, id maps, both CSR sides and both factor matrices resident on one GPU."""
 
@@ -239,11 +289,15 @@ class ALSCore:
             raise ValueError("ALS needs at least one rating")
         umin, umax = int(u.min()), int(u.max())
         imin, imax = int(i.min()), int(i.max())
-        if umin < 0 or imin < 0:
-            raise ValueError("user and item ids must be non-negative int32 values")
+        uoff, ioff = id_offset(umin, umax), id_offset(imin, imax)
+        if uoff:
+            u = (u.long() - uoff).to(torch.int32)
+        if ioff:
+            i = (i.long() - ioff).to(torch.int32)
         self.nnz = int(u.numel())
-        self.uidx = build_index(u, umax + 1, self.ws)
-        self.iidx = build_index(i, imax + 1, self.ws)
+        self.uidx = build_index(u, umax - uoff + 1, self.ws)
+        self.iidx = build_index(i, imax - ioff + 1, self.ws)
+        self.uidx.offset, self.iidx.offset = uoff, ioff
         self.user_block = build_block(u, self.uidx, i, self.iidx, r, self.ws, chunk)
         self.item_block = build_block(i, self.iidx, u, self.uidx, r, self.ws, chunk)
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
@@ -271,13 +325,15 @@ class ALSCore:
         idx = []
         for ids, F in ((user_ids, U), (item_ids, V)):
             ids = _to_device(ids, torch.int32, self.device)
-            if ids.numel() != F.shape[0] or ids.numel() == 0 or int(ids.min()) < 0:
-                raise ValueError("factor ids must be non-empty, non-negative and match the rows")
+            if ids.numel() != F.shape[0] or ids.numel() == 0:
+                raise ValueError("factor ids must be non-empty and match the rows")
             if ids.numel() > 1 and not bool((ids[1:] > ids[:-1]).all()):
                 raise ValueError("factor ids must be strictly ascending")
-            mp = torch.full((int(ids.max()) + 1,), -1, dtype=torch.int32, device=self.device)
-            mp[ids.long()] = torch.arange(ids.numel(), dtype=torch.int32, device=self.device)
-            idx.append(IdIndex(mp, ids.clone(), int(ids.numel())))
+            off = id_offset(int(ids.min()), int(ids.max()))
+            key = (ids.long() - off)
+            mp = torch.full((int(key.max()) + 1,), -1, dtype=torch.int32, device=self.device)
+            mp[key] = torch.arange(ids.numel(), dtype=torch.int32, device=self.device)
+            idx.append(IdIndex(mp, key.to(torch.int32), int(ids.numel()), off))
         self.uidx, self.iidx = idx
         self.rank = rank
         ld = ld_for(rank)
@@ -345,13 +401,17 @@ class ALSCore:
         self.check_status()
         return self
 
-    # ---- K4 / K5 ----
+    # ---- K4 / K5 (the serving protocol shared with distributed.ShardedALS) ----
     def predict(self, users, items) -> torch.Tensor:
+        """fp64 <u, v> per pair (MatrixFactorizationModel.predict's ddot); NaN where
+        either id is unknown."""
         u = _to_device(users, torch.int32, self.device)
         i = _to_device(items, torch.int32, self.device)
         return predict_pairs(u, i, self.uidx, self.iidx, self.U, self.V, self.rank)
 
     def rmse(self, users, items, ratings):
+        """(sqrt(sum (r - p)^2 / n), n) over the pairs whose ids are both known —
+        computeError (RecommenderSystem.py:103-129) fused into one pass."""
         u = _to_device(users, torch.int32, self.device)
         i = _to_device(items, torch.int32, self.device)
         r = _to_device(ratings, torch.float32, self.device)
@@ -359,19 +419,48 @@ class ALSCore:
                             self.ws).tolist()
         return (math.sqrt(sse / n) if n > 0 else float("nan")), int(n)
 
+    def _sides(self, user_side: bool):
+        if user_side:
+            return self.uidx, self.U, self.iidx, self.V
+        return self.iidx, self.V, self.uidx, self.U
+
+    def recommend_all(self, top: int, user_side: bool = True):
+        """recommendForAll: for every row of one side (dense order) its `top` best
+        rows of the other side.  Returns (keys [n], ids [n, t], scores [n, t]) on the
+        device, t = min(top, rows of the other side), scores descending."""
+        qi, Q, oi, Vo = self._sides(user_side)
+        idx, sc = topk_rows(Q, qi.n, Vo, oi.n, self.rank, top)
+        t = min(int(top), oi.n)
+        return qi.ids(), oi.ids()[idx[:, :t].long()], sc[:, :t]
+
+    def recommend_subset(self, ids, top: int, user_side: bool = True):
+        """recommendForUserSubset / ForItemSubset: distinct known ids of `ids`
+        (ascending) -> (keys, ids [m, t], scores [m, t])."""
+        qi, Q, oi, Vo = self._sides(user_side)
+        q = _to_device(ids, torch.int32, self.device)
+        keys = torch.unique(q)
+        rows = qi.rows_of(keys)
+        known = rows >= 0
+        keys, rows = keys[known], rows[known]
+        t = min(int(top), oi.n)
+        if keys.numel() == 0:
+            return keys, torch.empty((0, t), dtype=torch.int32, device=self.device), \
+                torch.empty((0, t), dtype=torch.float32, device=self.device)
+        Qs = Q.index_select(0, rows.long()).contiguous()
+        idx, sc = topk_rows(Qs, keys.numel(), Vo, oi.n, self.rank, top)
+        return keys, oi.ids()[idx[:, :t].long()], sc[:, :t]
+
     def recommend_users(self, top: int):
         """For every user (dense order): top items as (item ids, scores)."""
-        idx, sc = topk_rows(self.U, self.n_users, self.V, self.n_items, self.rank, top)
-        ids = torch.where(idx >= 0, self.iidx.uniq[idx.clamp(min=0).long()], idx)
+        _, ids, sc = self.recommend_all(top, True)
         return ids, sc
 
     def recommend_items(self, top: int):
-        idx, sc = topk_rows(self.V, self.n_items, self.U, self.n_users, self.rank, top)
-        ids = torch.where(idx >= 0, self.uidx.uniq[idx.clamp(min=0).long()], idx)
+        _, ids, sc = self.recommend_all(top, False)
         return ids, sc
 
     def user_factors(self):
-        return self.uidx.uniq, self.U[:, :self.rank]
+        return self.uidx.ids(), self.U[:, :self.rank]
 
     def item_factors(self):
-        return self.iidx.uniq, self.V[:, :self.rank]
+        return self.iidx.ids(), self.V[:, :self.rank]

@@ -112,10 +112,8 @@ class ALS(_Params):
         u = check_integers(u, p["userCol"])
         i = check_integers(i, p["itemCol"])
         r = to_float32(r)
-        if (u < 0).any() or (i < 0).any():
-            raise ValueError("this build requires non-negative user/item ids")
         seed = _DEFAULT_SEED if p["seed"] is None else int(p["seed"])
-        core = _engine.ALSCore(u, i, r)
+        core = _engine.make_engine(u, i, r)
         core.fit(int(p["rank"]), int(p["maxIter"]), float(p["regParam"]),
                  bool(p["implicitPrefs"]), float(p["alpha"]), seed=seed)
         return ALSModel(core, dict(p))
@@ -225,57 +223,37 @@ class ALSModel:
 
     # -- recommendForAll (K5) --
     def recommendForAllUsersArrays(self, numItems: int):
-        """Device tensors (user ids [n_u], item ids [n_u, numItems], scores [n_u, numItems])."""
-        ids, sc = self._core.recommend_users(int(numItems))
-        return self._core.uidx.uniq, ids, sc
+        """Device tensors (user ids [n_u], item ids [n_u, t], scores [n_u, t]),
+        t = min(numItems, n_items).  Multi-GPU: this rank's users (its partition)."""
+        return self._core.recommend_all(int(numItems), True)
 
     def recommendForAllItemsArrays(self, numUsers: int):
-        ids, sc = self._core.recommend_items(int(numUsers))
-        return self._core.iidx.uniq, ids, sc
+        return self._core.recommend_all(int(numUsers), False)
 
     @staticmethod
-    def _recs_df(key_col, rec_col, keys, ids, sc):
+    def _recs_df(key_col, keys, ids, sc):
         import pandas as pd
         keys = keys.cpu().numpy()
         ids = ids.cpu().numpy()
         sc = sc.cpu().numpy()
-        recs = [[(int(a), float(b)) for a, b in zip(ri, rs) if a >= 0] for ri, rs in zip(ids, sc)]
+        recs = [[(int(a), float(b)) for a, b in zip(ri, rs)] for ri, rs in zip(ids, sc)]
         return pd.DataFrame({key_col: keys, "recommendations": recs})
 
     def recommendForAllUsers(self, numItems: int):
-        """DataFrame[userCol, recommendations: list of (item, rating)] (rating desc)."""
-        keys, ids, sc = self.recommendForAllUsersArrays(numItems)
-        return self._recs_df(self._p["userCol"], self._p["itemCol"], keys, ids, sc)
+        """DataFrame[userCol, recommendations: list of (item, rating)], rating desc
+        (ties: lower item id first)."""
+        return self._recs_df(self._p["userCol"], *self.recommendForAllUsersArrays(numItems))
 
     def recommendForAllItems(self, numUsers: int):
-        keys, ids, sc = self.recommendForAllItemsArrays(numUsers)
-        return self._recs_df(self._p["itemCol"], self._p["userCol"], keys, ids, sc)
-
-    def _subset(self, dataset, col, idx, Q, V, n_v, uniq_other, num):
-        vals = columns_of(dataset, (col,))[0]
-        ids = np.unique(check_integers(vals, col))
-        mp = idx.map.cpu().numpy()
-        ok = (ids >= 0) & (ids < len(mp))
-        ids = ids[ok]
-        rows = mp[ids]
-        ids, rows = ids[rows >= 0], rows[rows >= 0]
-        core = self._core
-        if len(rows) == 0:
-            z = torch.empty((0, num), dtype=torch.int32)
-            return torch.as_tensor(ids), z, z.float()
-        Qs = Q.index_select(0, torch.as_tensor(rows, device=Q.device, dtype=torch.long))
-        di, sc = _engine.topk_rows(Qs.contiguous(), len(rows), V, n_v, core.rank, int(num))
-        out = torch.where(di >= 0, uniq_other[di.clamp(min=0).long()], di)
-        return torch.as_tensor(ids), out, sc
+        return self._recs_df(self._p["itemCol"], *self.recommendForAllItemsArrays(numUsers))
 
     def recommendForUserSubset(self, dataset, numItems: int):
-        c = self._core
-        keys, ids, sc = self._subset(dataset, self._p["userCol"], c.uidx, c.U, c.V, c.n_items,
-                                     c.iidx.uniq, numItems)
-        return self._recs_df(self._p["userCol"], None, keys, ids, sc)
+        """Top items for the distinct known users of `dataset[userCol]`."""
+        col = self._p["userCol"]
+        ids = check_integers(columns_of(dataset, (col,))[0], col)
+        return self._recs_df(col, *self._core.recommend_subset(ids, int(numItems), True))
 
     def recommendForItemSubset(self, dataset, numUsers: int):
-        c = self._core
-        keys, ids, sc = self._subset(dataset, self._p["itemCol"], c.iidx, c.V, c.U, c.n_users,
-                                     c.uidx.uniq, numUsers)
-        return self._recs_df(self._p["itemCol"], None, keys, ids, sc)
+        col = self._p["itemCol"]
+        ids = check_integers(columns_of(dataset, (col,))[0], col)
+        return self._recs_df(col, *self._core.recommend_subset(ids, int(numUsers), False))

@@ -110,36 +110,24 @@ class MatrixFactorizationModel:
         F = F.double().cpu().numpy()
         return [(int(a), tuple(row)) for a, row in zip(ids.cpu().numpy(), F)]
 
-    def _one(self, idx, Q, V, n_v, uniq_other, key, num, user_side):
-        mp = idx.map.cpu().numpy()
-        if key < 0 or key >= len(mp) or mp[key] < 0:
+    def _one(self, key, num, user_side):
+        keys, ids, sc = self._core.recommend_subset([int(key)], int(num), user_side)
+        if keys.numel() == 0:
             raise KeyError(f"unknown id {key}")
-        row = int(mp[key])
-        di, sc = _engine.topk_rows(Q[row:row + 1].contiguous(), 1, V, n_v, self._core.rank,
-                                   int(num))
-        di, sc = di.cpu().numpy()[0], sc.cpu().numpy()[0]
-        other = uniq_other.cpu().numpy()
-        out = []
-        for a, s in zip(di, sc):
-            if a < 0:
-                break
-            out.append(Rating(key, int(other[a]), float(s)) if user_side else
-                       Rating(int(other[a]), key, float(s)))
-        return out
+        ids, sc = ids.cpu().numpy()[0], sc.cpu().numpy()[0]
+        return [Rating(key, int(a), float(s)) if user_side else Rating(int(a), key, float(s))
+                for a, s in zip(ids, sc)]
 
     def recommendProducts(self, user: int, num: int) -> List[Rating]:
-        c = self._core
-        return self._one(c.uidx, c.U, c.V, c.n_items, c.iidx.uniq, int(user), num, True)
+        return self._one(int(user), num, True)
 
     def recommendUsers(self, product: int, num: int) -> List[Rating]:
-        c = self._core
-        return self._one(c.iidx, c.V, c.U, c.n_users, c.uidx.uniq, int(product), num, False)
+        return self._one(int(product), num, False)
 
     def recommendProductsForUsers(self, num: int):
-        ids, sc = self._core.recommend_users(int(num))
-        keys = self._core.uidx.uniq.cpu().numpy()
-        ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
-        return [(int(k), [Rating(int(k), int(a), float(s)) for a, s in zip(ri, rs) if a >= 0])
+        keys, ids, sc = self._core.recommend_all(int(num), True)
+        keys, ids, sc = keys.cpu().numpy(), ids.cpu().numpy(), sc.cpu().numpy()
+        return [(int(k), [Rating(int(k), int(a), float(s)) for a, s in zip(ri, rs)])
                 for k, ri, rs in zip(keys, ids, sc)]
 
     def save(self, sc, path: str, overwrite: bool = False) -> None:
@@ -159,10 +147,9 @@ class MatrixFactorizationModel:
                                                 V.astype(np.float32)))
 
     def recommendUsersForProducts(self, num: int):
-        ids, sc = self._core.recommend_items(int(num))
-        keys = self._core.iidx.uniq.cpu().numpy()
-        ids, sc = ids.cpu().numpy(), sc.cpu().numpy()
-        return [(int(k), [Rating(int(a), int(k), float(s)) for a, s in zip(ri, rs) if a >= 0])
+        keys, ids, sc = self._core.recommend_all(int(num), False)
+        keys, ids, sc = keys.cpu().numpy(), ids.cpu().numpy(), sc.cpu().numpy()
+        return [(int(k), [Rating(int(a), int(k), float(s)) for a, s in zip(ri, rs)])
                 for k, ri, rs in zip(keys, ids, sc)]
 
 
@@ -190,7 +177,7 @@ class ALS:
               ) -> MatrixFactorizationModel:
         _check(rank, iterations, lambda_, nonnegative)
         u, i, r = _triples(ratings)
-        core = _engine.ALSCore(u, i, r)
+        core = _engine.make_engine(u, i, r)
         core.fit(int(rank), int(iterations), float(lambda_), False, 1.0,
                  seed=_DEFAULT_SEED if seed is None else int(seed))
         return MatrixFactorizationModel(core)
@@ -201,7 +188,7 @@ class ALS:
                       seed: Optional[int] = None) -> MatrixFactorizationModel:
         _check(rank, iterations, lambda_, nonnegative, alpha)
         u, i, r = _triples(ratings)
-        core = _engine.ALSCore(u, i, r)
+        core = _engine.make_engine(u, i, r)
         core.fit(int(rank), int(iterations), float(lambda_), True, float(alpha),
                  seed=_DEFAULT_SEED if seed is None else int(seed))
         return MatrixFactorizationModel(core)

@@ -38,6 +38,28 @@ def rel_row_err(x, ref):
     return float((num / den).max())
 
 
+def row_len_buckets(indptr, err_rows, edges=(32, 128, 512, 2048)):
+    """Max per-row relative error bucketed by row length (ratings per row):
+    {"<=32": e, "33-128": e, ..., ">2048": e} (">2048" = heavy rows, chunked)."""
+    deg = np.diff(np.asarray(indptr))
+    lo = 0
+    out = {}
+    for hi in list(edges) + [None]:
+        sel = deg > lo if hi is None else (deg > lo) & (deg <= hi)
+        name = f">{lo}" if hi is None else (f"<={hi}" if lo == 0 else f"{lo + 1}-{hi}")
+        out[name] = {"rows": int(sel.sum()), "max_rel_err": float(err_rows[sel].max()) if sel.any()
+                     else None}
+        lo = hi if hi is not None else lo
+    return out
+
+
+def rel_row_errs(x, ref):
+    """Per-row ||x - ref|| / ||ref|| (vector)."""
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return np.linalg.norm(x - ref, axis=1) / np.maximum(np.linalg.norm(ref, axis=1), 1e-6)
+
+
 def report(name, value):
     """Append a measured error to $ALS_TEST_REPORT (JSON lines) when set."""
     import json
@@ -45,4 +67,28 @@ def report(name, value):
     path = os.environ.get("ALS_TEST_REPORT")
     if path:
         with open(path, "a") as f:
-            f.write(json.dumps({"test": name, "value": float(value)}) + "\n")
+            v = value if isinstance(value, (dict, list)) else float(value)
+            f.write(json.dumps({"test": name, "value": v}) + "\n")
+
+
+def oracle_train_c(users, items, ratings, rank, iterations, reg, U0, implicit=False, alpha=1.0):
+    """ALS.train restated (oracle.als_oracle's loop) with the C half-sweeps
+    (oracle/als_oracle.c, OpenMP) for the larger parity cases.
+    Returns (U, V, umap, imap, uids, iids)."""
+    from oracle import als_oracle as O
+    from oracle import c_oracle as C
+    users = np.asarray(users, np.int64)
+    items = np.asarray(items, np.int64)
+    ratings = np.asarray(ratings, np.float32)
+    umap, uids = O.index_build(users, int(users.max()) + 1)
+    imap, iids = O.index_build(items, int(items.max()) + 1)
+    ip = O.csr_build(imap[items], umap[users], ratings, len(iids))
+    up = O.csr_build(umap[users], imap[items], ratings, len(uids))
+    U = np.asarray(U0, np.float32)
+    V = np.zeros((len(iids), rank), np.float32)
+    for _ in range(iterations):
+        V, st = C.half_sweep(*ip, U, reg, implicit=implicit, alpha=alpha)
+        assert not st.any()
+        U, st = C.half_sweep(*up, V, reg, implicit=implicit, alpha=alpha)
+        assert not st.any()
+    return U, V, umap, imap, uids, iids

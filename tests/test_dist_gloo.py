@@ -46,6 +46,26 @@ class OracleKernels:
         x = self.O.solve(A, b, ne, reg, None if yty is None else yty.numpy())
         X[:n, :rank] = torch.as_tensor(x)
 
+    def predict(self, u_keys, i_keys, umap, imap, U, V, rank):
+        u, i = u_keys.long(), i_keys.long()
+        ok = (u >= 0) & (i >= 0)
+        ur = torch.where(ok, umap[u.clamp(min=0)].long(), -1)
+        ir = torch.where(ok, imap[i.clamp(min=0)].long(), -1)
+        ok = ok & (ur >= 0) & (ir >= 0)
+        out = torch.full((len(u),), float("nan"), dtype=torch.float64)
+        out[ok] = (U[ur[ok], :rank].double() * V[ir[ok], :rank].double()).sum(1)
+        return out
+
+    def rmse_partial(self, u_keys, i_keys, r, umap, imap, U, V, rank):
+        p = self.predict(u_keys, i_keys, umap, imap, U, V, rank)
+        ok = ~torch.isnan(p)
+        d = r.double()[ok] - p[ok]
+        return torch.tensor([float((d * d).sum()), float(ok.sum())], dtype=torch.float64)
+
+    def topk(self, Q, n_q, V, n_v, rank, top):
+        i, s = self.O.topk(Q[:n_q, :rank].numpy(), V[:n_v, :rank].numpy(), top)
+        return torch.as_tensor(i), torch.as_tensor(s, dtype=torch.float32)
+
     def ld(self, rank):
         return rank
 
@@ -87,6 +107,78 @@ def _worker(rank, world, port, implicit, chunks, out_dir):
                  u_starts=K.users.starts.numpy(), i_starts=K.items.starts.numpy(),
                  local=[K.user_rows, K.item_rows])
     dist.destroy_process_group()
+
+
+def _serve_worker(rank, world, port, out_dir):
+    """Seeded fit (no explicit U0) + rmse / predict / recommendForAll on world ranks."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x.distributed import ShardedALS
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r = planted(90, 70, density=0.1, seed=31, heavy_items=(2,))
+    u = (u - 40).astype(np.int32)  # negative user ids are legal (Spark Int ids)
+    sel = np.arange(len(u)) % world == rank
+    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
+    K.fit(5, 2, 0.1, seed=11)
+    rm, n = K.rmse(u[sel], i[sel], r[sel])  # every rank passes its own pairs
+    q_u = np.array([u[0], u[1], 10 ** 6, -(10 ** 6)], np.int32)
+    q_i = np.array([i[0], i[1], i[2], i[3]], np.int32)
+    pred = K.predict(q_u, q_i).numpy()
+    keys, ids, sc = K.recommend_all(7, True)
+    skeys, sids, ssc = K.recommend_subset(np.array([i[5], i[5], 10 ** 7], np.int32), 4, False)
+    uid, Uf = K.user_factors()
+    iid, Vf = K.item_factors()
+    np.savez(os.path.join(out_dir, f"serve_{world}_{rank}.npz"), rmse=rm, n=n, pred=pred,
+             keys=keys.numpy(), ids=ids.numpy(), sc=sc.numpy(), skeys=skeys.numpy(),
+             sids=sids.numpy(), ssc=ssc.numpy(), uid=uid.numpy(), U=Uf.numpy(),
+             iid=iid.numpy(), V=Vf.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_serving_matches_oracle(tmp_path, world):
+    """Seeded init over the global dense rows (independent of world size), the
+    distributed RMSE (all_reduce of the fused partials), predict on replicated
+    factors, and recommendForAll over each rank's own users, vs a single-process
+    oracle fit from the same seeded start."""
+    mp.spawn(_serve_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    from oracle import als_oracle as O
+    u, i, r = planted(90, 70, density=0.1, seed=31, heavy_items=(2,))
+    u = (u - 40).astype(np.int32)
+    n_users = len(np.unique(u))
+    g = torch.Generator(device="cpu")
+    g.manual_seed(11)
+    x = torch.randn((n_users, 5), generator=g, dtype=torch.float32)
+    U0 = (x / torch.linalg.vector_norm(x, dim=1, keepdim=True)).numpy()
+    U, V, umap, imap, uids, iids = O.train(u + 40, i, r, 5, 2, 0.1, U0=U0)
+    uids = uids - 40
+    sse, n_ref = O.rmse(U, V, umap, imap, u + 40, i, r)
+    parts = [np.load(tmp_path / f"serve_{world}_{w}.npz") for w in range(world)]
+    for d in parts:
+        np.testing.assert_array_equal(d["uid"], uids)
+        np.testing.assert_allclose(d["U"], U, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(d["V"], V, rtol=1e-5, atol=1e-6)
+        assert int(d["n"]) == n_ref == len(u)
+        assert abs(float(d["rmse"]) - np.sqrt(sse / n_ref)) <= 1e-9
+        assert np.isnan(d["pred"][2:]).all() and not np.isnan(d["pred"][:2]).any()
+    # recommendForAll: the union of the ranks' partitions is every user exactly once
+    keys = np.concatenate([d["keys"] for d in parts])
+    ids = np.concatenate([d["ids"] for d in parts])
+    np.testing.assert_array_equal(np.sort(keys), uids)
+    ref_i, ref_s = O.topk(U, V, 7)
+    order = np.argsort(keys)
+    np.testing.assert_array_equal(ids[order], iids[ref_i])
+    d = parts[0]
+    assert list(d["skeys"]) == [i[5]]
+    row = int(np.searchsorted(iids, i[5]))
+    ref_u, _ = O.topk(V[row:row + 1], U, 4)
+    np.testing.assert_array_equal(d["sids"][0], uids[ref_u[0]])
 
 
 @pytest.mark.parametrize("implicit,chunks", [(False, None), (True, None), (False, 3), (True, 3)])

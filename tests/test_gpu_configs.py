@@ -1,0 +1,160 @@
+"""Parity at the benchmarked configurations, through the production path.
+
+Every call here uses the engine's defaults — DEFAULT_CHUNK (2048-rating tasks,
+fp32 accumulation inside a task, fp64 across a heavy row's chunks) and the
+bench's data generator — so the arithmetic checked is the arithmetic
+`bench.py` times (BASELINE.json configs[0]-[2]):
+
+  * configs[0] (ml-latest-small shape, 610 x 9,724, 100,836 ratings, rank 10,
+    maxIter 10, regParam 0.1): a full 10-iteration fit, factors compared with
+    the oracle after EVERY iteration (north_star: 1e-4 relative per iteration),
+    then the RMSE (1e-4).
+  * configs[1] (ML-25M shape, 25,000,095 ratings, rank 64) and configs[2] (same
+    data, implicit alpha = 40, rank 128): one item and one user half-sweep from
+    identical source factors against the C restatement of Spark's dspr + dppsv
+    (oracle/als_oracle.c), max per-row relative error <= 1e-4, reported by row
+    length so the 2048-rating fp32 tasks and the chunked heavy rows are visible;
+    K1's CSR at full size bit-exact against the numpy oracle.
+  * top-10 of recommendForAllUsers for a 2,000-user sample at configs[1]
+    against the fp64 oracle (identical except fp ties within 1e-5).
+
+Reference call sites: RecommenderSystem.py:148-150 (ALS.train -> predictAll).
+"""
+import numpy as np
+import pytest
+import torch
+
+import als_mi355x.datasets as D
+import als_mi355x.engine as E
+from helpers import rel_row_errs, report, row_len_buckets
+from oracle import als_oracle as O
+from oracle import c_oracle as C
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+TOL = 1e-4  # north_star: factors within 1e-4 relative per iteration
+
+
+def _host_csr(block):
+    return (block.row_ptr.cpu().numpy(), block.col.cpu().numpy(), block.val.cpu().numpy())
+
+
+def test_configs0_full_fit_per_iteration():
+    """configs[0]: 10 iterations, compared after each one (the production chunk)."""
+    u, i, r = (t.cpu().numpy() for t in D.synthetic_config("ml_latest_small", device=DEV))
+    rank, iters, reg = 10, 10, 0.1
+    core = E.ALSCore(u, i, r, device=DEV)
+    assert core.item_block.chunk == E.DEFAULT_CHUNK
+    core.init_factors(rank, seed=5)
+    U_ref = core.U[:, :rank].cpu().numpy().copy()
+    umap, uids = O.index_build(u, int(u.max()) + 1)
+    imap, iids = O.index_build(i, int(i.max()) + 1)
+    ip = O.csr_build(imap[i], umap[u], r, len(iids))
+    up = O.csr_build(umap[u], imap[i], r, len(uids))
+    worst = 0.0
+    for it in range(iters):
+        core.iterate(reg)
+        V_ref, st = C.half_sweep(*ip, U_ref, reg)
+        assert not st.any()
+        U_ref, st = C.half_sweep(*up, V_ref, reg)
+        assert not st.any()
+        ev = rel_row_errs(core.V[:, :rank].cpu().numpy(), V_ref).max()
+        eu = rel_row_errs(core.U[:, :rank].cpu().numpy(), U_ref).max()
+        worst = max(worst, ev, eu)
+        assert ev <= TOL and eu <= TOL, f"iteration {it + 1}: item {ev:.2e} user {eu:.2e}"
+    core.check_status()
+    report("configs0_fit_max_rel_err_over_10_iterations", worst)
+    rm, n = core.rmse(u, i, r)
+    sse, n_ref = O.rmse(U_ref, V_ref, umap, imap, u, i, r)
+    assert n == n_ref == len(u)
+    assert abs(rm - np.sqrt(sse / n_ref)) <= TOL
+
+
+@pytest.fixture(scope="module")
+def ml25m():
+    u, i, r = D.synthetic_config("ml25m", device=DEV)
+    core = E.ALSCore(u, i, r, device=DEV)
+    host = (u.cpu().numpy(), i.cpu().numpy(), r.cpu().numpy())
+    del u, i, r
+    return core, host
+
+
+def test_configs1_csr_full_size_bitexact(ml25m):
+    core, (u, i, r) = ml25m
+    umap, uids = O.index_build(u, int(u.max()) + 1)
+    imap, iids = O.index_build(i, int(i.max()) + 1)
+    np.testing.assert_array_equal(core.uidx.uniq.cpu().numpy(), uids)
+    np.testing.assert_array_equal(core.iidx.uniq.cpu().numpy(), iids)
+    for block, rows, cols, n in ((core.item_block, imap[i], umap[u], len(iids)),
+                                 (core.user_block, umap[u], imap[i], len(uids))):
+        ptr_, idx_, val_ = O.csr_build(rows, cols, r, n)
+        np.testing.assert_array_equal(block.row_ptr.cpu().numpy(), ptr_)
+        np.testing.assert_array_equal(block.col.cpu().numpy(), idx_)
+        np.testing.assert_array_equal(block.val.cpu().numpy(), val_)
+
+
+def _half_sweeps(core, rank, implicit, alpha, tag):
+    reg = 0.1
+    core.init_factors(rank, seed=5)
+    U0 = core.U[:, :rank].cpu().numpy()
+    core.status.zero_()
+    core.half_sweep_items(reg, implicit, alpha)
+    torch.cuda.synchronize()
+    core.check_status()
+    ip = _host_csr(core.item_block)
+    V_ref, st = C.half_sweep(*ip, U0, reg, implicit=implicit, alpha=alpha)
+    assert not st.any()
+    V = core.V.cpu().numpy()
+    assert np.all(V[:, rank:] == 0.0)
+    ev = rel_row_errs(V[:, :rank], V_ref)
+    report(f"{tag}_item_half_sweep_by_row_length", row_len_buckets(ip[0], ev))
+    assert ev.max() <= TOL, row_len_buckets(ip[0], ev)
+    # user side from the oracle's V (identical source factors)
+    core.V[:, :rank] = torch.as_tensor(V_ref).to(DEV)
+    core.half_sweep_users(reg, implicit, alpha)
+    torch.cuda.synchronize()
+    core.check_status()
+    up = _host_csr(core.user_block)
+    U_ref, st = C.half_sweep(*up, V_ref, reg, implicit=implicit, alpha=alpha)
+    assert not st.any()
+    eu = rel_row_errs(core.U[:, :rank].cpu().numpy(), U_ref)
+    report(f"{tag}_user_half_sweep_by_row_length", row_len_buckets(up[0], eu))
+    assert eu.max() <= TOL, row_len_buckets(up[0], eu)
+    # the bench shape really exercises long fp32 tasks and chunked heavy rows
+    assert (np.diff(ip[0]) > 1024).sum() > 100 and core.item_block.n_chunks > 1000
+
+
+def test_configs1_half_sweeps_rank64(ml25m):
+    core, _ = ml25m
+    _half_sweeps(core, 64, False, 1.0, "configs1_rank64")
+
+
+def test_configs2_half_sweeps_rank128_implicit(ml25m):
+    core, _ = ml25m
+    _half_sweeps(core, 128, True, 40.0, "configs2_rank128_implicit")
+
+
+def test_configs1_top10_sample(ml25m):
+    """recommendForAllUsers(10) rows of a 2,000-user sample vs the fp64 oracle."""
+    core, _ = ml25m
+    rank = 64
+    core.init_factors(rank, seed=5)
+    for _ in range(2):
+        core.iterate(0.1)
+    idx, sc = E.topk_rows(core.U, core.n_users, core.V, core.n_items, rank, 10)
+    rng = np.random.default_rng(7)
+    rows = np.sort(rng.choice(core.n_users, 2000, replace=False))
+    U = core.U[:, :rank].cpu().numpy()
+    V = core.V[:, :rank].cpu().numpy()
+    ref_i, ref_s = O.topk(U[rows], V, 10)
+    got_i = idx.cpu().numpy()[rows]
+    got_s = sc.cpu().numpy()[rows]
+    S = U[rows].astype(np.float64) @ V.astype(np.float64).T
+    mism = 0
+    for t in range(len(rows)):
+        bad = np.nonzero(got_i[t] != ref_i[t])[0]
+        for p in bad:
+            mism += 1
+            assert abs(S[t, got_i[t, p]] - ref_s[t, p]) <= 1e-5 * max(1.0, abs(ref_s[t, p]))
+    np.testing.assert_allclose(got_s, ref_s, rtol=1e-5, atol=1e-5)
+    report("configs1_top10_sample_tie_swaps", mism)

@@ -112,7 +112,15 @@ struct FullTiles {
   // [0, ld): lanes whose dims are >= k read real dims, masked out after the Gram).
   __device__ static __forceinline__ void load_clamped(const float* __restrict__ row,
                                                       float (&y)[NC], int d0, int ld) {
-    load_dims<CN>(row + (d0 + CN <= ld ? d0 : ld - CN), y);
+    if constexpr (CN == 8) {
+      auto cl = [&](int o) { return o + 4 <= ld ? o : ld - 4; };
+      const float4 a = *reinterpret_cast<const float4*>(row + cl(d0));
+      const float4 b = *reinterpret_cast<const float4*>(row + cl(d0 + 4));
+      y[0] = a.x; y[1] = a.y; y[2] = a.z; y[3] = a.w;
+      y[4] = b.x; y[5] = b.y; y[6] = b.z; y[7] = b.w;
+    } else {
+      load_dims<CN>(row + (d0 + CN <= ld ? d0 : ld - CN), y);
+    }
   }
   // This lane's NC words of a pre-split row (p = row + m*CN; rows are kp = 16*CN wide).
   __device__ static __forceinline__ void load_pre(const uint32_t* __restrict__ p,
@@ -122,10 +130,15 @@ struct FullTiles {
     } else if constexpr (CN == 2) {
       const uint2 v = *reinterpret_cast<const uint2*>(p);
       w[0] = v.x; w[1] = v.y;
-    } else {
-      static_assert(CN == 4, "pre-split rows: CN in {1, 2, 4}");
+    } else if constexpr (CN == 4) {
       const uint4 v = *reinterpret_cast<const uint4*>(p);
       w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    } else {
+      static_assert(CN == 8, "pre-split rows: CN in {1, 2, 4, 8}");
+      const uint4 a = *reinterpret_cast<const uint4*>(p);
+      const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
+      w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+      w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
     }
   }
 };
@@ -1001,9 +1014,249 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
   return ok;
 }
 
+
+// ---------------------------------------------------------------------------
+// k in (64, 128]: ONE wavefront per system ("W1"), block Gaussian elimination
+// with explicit inverses of the 16 x 16 diagonal blocks (NB = 8 block rows).
+//
+// The Gram's 36 upper tiles stay in the MFMA C layout (lane (q, m): rows
+// 4q..4q+3 of column m).  For two tiles X, Y in that layout, the products
+//   C += X^T Y  =  sum_s4 mfma_16x16x4_f32(X.reg[s4], Y.reg[s4])
+// need no data movement (the MFMA's k index is permuted to 4q + s4), so the
+// whole right-looking elimination runs on registers:
+//   for K = 0..7:
+//     Gm   = -(B_KK)^-1            sweep operator on the diagonal block (VALU,
+//                                  column per lane, lane-p broadcasts by DPP)
+//     Pm_J = Gm B_KJ   (J > K)     = -B_KK^-1 B_KJ, on the matrix cores
+//     B_IJ += B_KI^T Pm_J (K < I <= J)   Schur complement, matrix cores
+//     b_J  += Pm_J^T b_K,  z_K = -Gm b_K
+//     tile (K, J) <- Pm_J           (kept for the back substitution)
+//   x_K = z_K + sum_{J>K} Pm_KJ x_J,  K = 7..0.
+// The sweep's pivots are the LDL^T pivots of B (all must be > 0: Spark's dppsv
+// fails otherwise).  Same solution as Spark's Cholesky dppsv, fp32 arithmetic
+// with exact-product fp32 MFMA; no barrier, no LDS beyond one 16 x 16
+// transposition buffer per wave.
+// rhs layouts: "column" = lane m (any q) holds element m of a 16-block;
+// "row" = lanes of row-group q hold elements 4q..4q+3.
+// ---------------------------------------------------------------------------
+struct W1Lds {
+  static constexpr int CS = 20;                     // floats per column (16 + pad, 16-B aligned)
+  // transposition buffer | rhs vector | Pm tiles of the back substitution (28 x 256)
+  static constexpr int COL = 0, VEC = 16 * CS, PM = VEC + 16, SIZE = PM + 28 * 256;
+};
+
+constexpr int kW1NB = 8;
+
+__host__ __device__ constexpr int w1_tile(int i, int j) { return tile_index(kW1NB, i, j); }
+
+// v on lanes with (lane & 15) == P, else w (mask from the scalar unit).
+template <int P>
+__device__ __forceinline__ float sel_lane16(float v, float w) {
+  float r;
+  const uint64_t msk = 0x0001000100010001ull << P;
+  asm volatile("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(v), "v"(w), "s"(msk));
+  return r;
+}
+
+// Sum over the four 16-lane row groups (every lane gets the total): two VALU
+// row swaps (v_permlane16_swap: rows 0<->1, 2<->3; v_permlane32_swap: rows
+// {0,1}<->{2,3}), no LDS crossbar on the dependency chain.
+// (Inline asm: this compiler's __builtin_amdgcn_permlane*_swap loses the second
+// result when both are consumed — measured, it emitted v_add v1, v1, v1.)
+__device__ __forceinline__ float reduce_rows4(float v) {
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  float c = a + b, d = c;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
+  return c + d;
+}
+
+// Sum over the 16 lanes of each row group (every lane of the group gets it).
+// Lane P of each 16-lane row, as a DPP source the combiner folds into the user
+// (bound_ctrl set, old undefined: v_fmac_f32_dpp / v_rcp_f32_dpp row_newbcast:P).
+template <int P>
+__device__ __forceinline__ float bcast16(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + P,
+                                                            0xF, 0xF, true));
+}
+
+// r += (lane P's r, same 16-lane row) * nf: one v_fmac_f32_dpp row_newbcast:P.
+template <int P>
+__device__ __forceinline__ void fmac_bcast16(float& r, float nf) {
+  asm volatile("v_fmac_f32_dpp %0, %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+               : "+v"(r)
+               : "v"(nf), "i"(P));
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL,
+                                                               0xF, 0xF, false));
+}
+
+__device__ __forceinline__ float reduce_lanes16(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return v;
+}
+
+// Sweep operator over all 16 pivots of a symmetric 16 x 16 block held column per
+// lane (R[i] = B[i][m], replicated in the four row groups): R <- -(B^-1) column m.
+// Pivot p: d = B[p][p]; B[i][j] -= B[i][p] B[p][j] / d; row/column p scaled by
+// 1/d; B[p][p] = -1/d.  The pivot column's 1/d scaling is DEFERRED: lane p keeps
+// its column unscaled (multiplier 0 at its own pivot) and every column is scaled
+// by 1/(its pivot) once at the end.  The stored values then follow the generic
+// update for every lane (the multiplier -B[p][m]/d does not depend on a column's
+// pending scale), and no lane ever forms 1 - 1/d (which cancels for large d).
+// Returns the smallest pivot (> 0 for an SPD block; NaN propagates as "not > 0").
+__device__ __forceinline__ float sweep16(float (&R)[16]) {
+  float dmin = 3.0e38f;  // NaN pivots are not seen here: they make the solution NaN
+  float dself = 1.f;     // this lane's own pivot (its column's deferred scale is 1/dself)
+  static_for<16>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    const float d = bcast16<p>(R[p]);
+    dmin = fminf(dmin, d);
+    const float rd = rcp_t(d);
+    const float f = R[p] * rd;
+    const float nf = sel_lane16<p>(0.f, -f);
+    // R[i] += (lane p's R[i]) * nf as ONE v_fmac_f32_dpp per row (the compiler only
+    // folds DPP into untied VOP2 ops); s_nop 1 covers the VALU-write -> DPP-read
+    // hazard of the previous pivot's last writes.
+    asm volatile("s_nop 1" ::: "memory");
+    static_for<16>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i != p) fmac_bcast16<p>(R[i], nf);
+    });
+    R[p] = sel_lane16<p>(-1.f, f);
+    dself = sel_lane16<p>(d, dself);
+  });
+  const float s = rcp_t(dself);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) R[i] *= s;
+  return dmin;
+}
+
+template <int NT>
+__device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
+                                         float* __restrict__ lds, int k,
+                                         float* __restrict__ xrow, int ld) {
+  static_assert(NT == kW1NB * (kW1NB + 1) / 2, "36 upper tiles");
+  constexpr int NB = kW1NB, CS = W1Lds::CS;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  float* col = lds + W1Lds::COL;
+  float* vec = lds + W1Lds::VEC;
+  float zcol[NB];
+  float dmin = 3.0e38f;
+  // bcol[J] for J > 0 holds per-row-group partial sums (summed over the groups when
+  // block J becomes the pivot block): start with the full b_J in row group 0
+#pragma unroll
+  for (int c = 1; c < NB; ++c) bcol[c] = q == 0 ? bcol[c] : 0.f;
+  static_for<NB>([&](auto Kc) {
+    constexpr int K = decltype(Kc)::value;
+    // (1) diagonal block: C layout -> column per lane (LDS), sweep, -> C layout
+    *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile(K, K)];
+    wave_lds_sync();
+    float R[16];
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * c4);
+      R[4 * c4] = v[0]; R[4 * c4 + 1] = v[1]; R[4 * c4 + 2] = v[2]; R[4 * c4 + 3] = v[3];
+    }
+    dmin = fminf(dmin, sweep16(R));
+    wave_lds_sync();
+    const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
+    if (q == 0) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        *reinterpret_cast<floatx4*>(col + m * CS + 4 * c4) =
+            floatx4{R[4 * c4], R[4 * c4 + 1], R[4 * c4 + 2], R[4 * c4 + 3]};
+      vec[m] = bK;
+    }
+    wave_lds_sync();
+    const floatx4 Gm = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * q);  // C layout
+    const floatx4 bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);          // row layout
+    wave_lds_sync();
+    // z_K = -Gm b_K  (Gm symmetric: (Gm b)[i] = sum_k Gm[k][i] b[k])
+    zcol[K] = -reduce_rows4(Gm[0] * bk[0] + Gm[1] * bk[1] + Gm[2] * bk[2] + Gm[3] * bk[3]);
+    if constexpr (K + 1 < NB) {
+      // (2) Pm_J = Gm B_KJ;  b_J += Pm_J^T b_K
+      floatx4 Pm[NB - 1 - K];
+      static_for<NB - 1 - K>([&](auto jc) {
+        constexpr int J = K + 1 + decltype(jc)::value;
+        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Gm[s4], A[w1_tile(K, J)][s4], acc, 0, 0, 0);
+        Pm[decltype(jc)::value] = acc;
+        // b_J += Pm_J^T b_K, kept as per-row-group partials until J is the pivot block
+        bcol[J] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
+      });
+      // (3) Schur complement B_IJ += B_KI^T Pm_J, K < I <= J
+      static_for<NB - 1 - K>([&](auto ic) {
+        constexpr int I = K + 1 + decltype(ic)::value;
+        static_for<NB - I>([&](auto jc) {
+          constexpr int J = I + decltype(jc)::value;
+          floatx4 acc = A[w1_tile(I, J)];
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[w1_tile(K, I)][s4], Pm[J - K - 1][s4],
+                                                        acc, 0, 0, 0);
+          A[w1_tile(I, J)] = acc;
+        });
+      });
+      // (4) Pm of block row K -> LDS for the back substitution (lane-private slots)
+      static_for<NB - 1 - K>([&](auto jc) {
+        constexpr int J = K + 1 + decltype(jc)::value;
+        *reinterpret_cast<floatx4*>(lds + W1Lds::PM + (w1_tile(K, J) - (K + 1)) * 256 + 4 * lane) =
+            Pm[decltype(jc)::value];
+      });
+    }
+  });
+  // back substitution x_K = z_K + sum_{J>K} Pm_KJ x_J (column layout)
+  float xcol[NB];
+  xcol[NB - 1] = zcol[NB - 1];
+  static_for<NB - 1>([&](auto kc) {
+    constexpr int K = NB - 2 - decltype(kc)::value;
+    float pr[4] = {0.f, 0.f, 0.f, 0.f};
+    static_for<NB - 1 - K>([&](auto jc) {
+      constexpr int J = K + 1 + decltype(jc)::value;
+      const floatx4 pm = *reinterpret_cast<const floatx4*>(
+          lds + W1Lds::PM + (w1_tile(K, J) - (K + 1)) * 256 + 4 * lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pr[r] = fmaf(pm[r], xcol[J], pr[r]);
+    });
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pr[r] = reduce_lanes16(pr[r]);  // rows 4q+r of Pm x
+    if (m == 0) *reinterpret_cast<floatx4*>(vec + 4 * q) = floatx4{pr[0], pr[1], pr[2], pr[3]};
+    wave_lds_sync();
+    xcol[K] = zcol[K] + vec[m];
+    wave_lds_sync();
+  });
+  // a NaN pivot (or overflow) leaves a non-finite solution
+  bool fin = true;
+#pragma unroll
+  for (int c = 0; c < NB; ++c) fin = fin && (xcol[c] - xcol[c] == 0.f);
+  const bool ok = dmin > 0.f && __ballot(!fin) == 0;
+  // un-permute: dim d = i * 8 + c  <->  block c, index i = lane m
+  if (lane < 16) {
+#pragma unroll
+    for (int c = 0; c < NB; ++c) {
+      const int d = m * NB + c;
+      if (d < ld) xrow[d] = (d < k && ok) ? xcol[c] : 0.f;
+    }
+  }
+  return ok;
+}
+
 template <int CN>
 struct SmemBytes {
   static constexpr int value = (int)sizeof(float) * PanelLds<CN>::SIZE;
+};
+template <>
+struct SmemBytes<8> {  // W1: transposition buffer (the Gram's 128-word staging fits in it)
+  static constexpr int value = (int)sizeof(float) * W1Lds::SIZE;
 };
 
 __device__ __forceinline__ float shfl_xor_t(float v, int m) { return __shfl_xor(v, m); }
@@ -1232,6 +1485,211 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
   finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
                                          X + (int64_t)row * ld, ld, row, status);
+}
+
+// ---------------------------------------------------------------------------
+// W1 kernels (k in (64, 128], one wavefront per system).  The 36 scaled Gram
+// tiles are finished in place, tile by tile (regularisation, implicit YtY from
+// a C-layout fp32 table, identity rows for padded dims), so the register file
+// holds one copy of the system.  Heavy-row chunk partials are stored as fp32
+// (a chunk's sum is fp32 anyway) and summed in fp64 in launch 2, where the YtY
+// merge is done in fp64 before the single rounding.
+// ---------------------------------------------------------------------------
+constexpr int kW1NT = 36;
+constexpr int kW1Slot = (kW1NT * 4 + kW1NB + 1) * 64;  // floats per chunk partial
+constexpr int kW1YtyC = kW1NT * 4 * 64;               // floats of the C-layout YtY table
+
+// ytyC[(t * 4 + r) * 64 + lane] = fp32 YtY entry of register r of upper tile t.
+__global__ __launch_bounds__(64) void yty_ctab_kernel(const double* __restrict__ yty,
+                                                      float* __restrict__ ytyC) {
+  static_for<kW1NT>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    constexpr int c1 = FullTiles<8>::l1(t), c2 = FullTiles<8>::l2(t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int i, j;
+      tile_ij<8>(c1, c2, r, i, j);
+      const int hi = i > j ? i : j, lo = i > j ? j : i;
+      ytyC[(t * 4 + r) * 64 + threadIdx.x] = (float)yty[hi * (hi + 1) / 2 + lo];
+    }
+  });
+}
+
+// Completes the normal equations of one system in place and solves them.  A holds
+// the Gram divided by `scale` (the split MFMA's power-of-two scaling, 1 for the
+// reduced heavy rows); instead of rescaling 144 registers, the system is solved
+// in that scale: (A + (lambda n / scale) I) x = b / scale  (+ YtY / scale for
+// implicit, from the C-layout table).  Padded dims (k < 128) become identity
+// rows/columns.  bt: per-lane rhs partials (summed over the 4 rating slots here).
+template <bool ADD_YTY>
+__device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[kW1NT], float scale,
+                                                    float (&bt)[kW1NB], int64_t n_reg,
+                                                    const float* __restrict__ ytyC,
+                                                    unsigned char* smem, int k, float reg,
+                                                    float* __restrict__ xrow, int ld, int row,
+                                                    int32_t* __restrict__ status) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const float inv = 1.f / scale;  // power of two: exact
+  float bq[kW1NB];
+#pragma unroll
+  for (int c = 0; c < kW1NB; ++c) {
+    const float v = reduce_rows4(bt[c]) * inv;
+    bq[c] = m * kW1NB + c < k ? v : 0.f;
+  }
+  const float lam = (float)((double)reg * (double)n_reg) * inv;
+  if constexpr (ADD_YTY) {
+    static_for<kW1NT>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[t][r] = fmaf(ytyC[(t * 4 + r) * 64 + lane], inv, A[t][r]);
+    });
+  }
+  if (k == kW1NB * 16) {  // uniform: no padded dims, lambda on the diagonal only
+    static_for<kW1NB>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      constexpr int t = w1_tile(c, c);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A[t][r] += (4 * q + r == m) ? lam : 0.f;
+    });
+  } else {
+    static_for<kW1NT>([&](auto tc) {
+      constexpr int t = decltype(tc)::value;
+      constexpr int c1 = FullTiles<8>::l1(t), c2 = FullTiles<8>::l2(t);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int i, j;
+        tile_ij<8>(c1, c2, r, i, j);
+        const bool pad = (i >= k) | (j >= k);
+        float v = pad ? 0.f : A[t][r];
+        if constexpr (c1 == c2) v = (i == j) ? (pad ? 1.f : v + lam) : v;
+        A[t][r] = v;
+      }
+    });
+  }
+  const bool ok = w1_solve<kW1NT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
+}
+
+// Launch 1 (W1): heavy-row chunks (-> fp32 partial slots) and whole light rows
+// (Gram + solve fused), as gram_solve_kernel.  ytyC: C-layout YtY (implicit).
+template <bool IMPLICIT>
+__global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
+    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
+    int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
+    int k, float reg, float alpha, const float* __restrict__ ytyC, float* __restrict__ slots,
+    int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
+    int32_t kp, int32_t zero_row) {
+  constexpr int CN = 8, NT = kW1NT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  const int lane = threadIdx.x & 63;
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bt[CN];
+#pragma unroll
+  for (int c = 0; c < CN; ++c) bt[c] = 0.f;
+  int npos = 0;
+  int chunk, light;
+  decode_task(blockIdx.x, n_chunks, n_light, chunk, light);
+  int64_t pb, pe;
+  int row = -1;
+  if (chunk >= 0) {
+    pb = chunk_begin[chunk];
+    pe = chunk_end[chunk];
+  } else {
+    row = light_rows[light];
+    pb = row_ptr[row];
+    pe = row_ptr[row + 1];
+  }
+  float inv2;
+  if constexpr (IMPLICIT) {
+    const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
+    inv2 = ldexpf(1.f, -2 * e);
+    gram_accumulate_split<CN, true>(col, val, pb, pe, Y, ld, k, alpha, ldexpf(1.f, e), acc, bt,
+                                    npos, reinterpret_cast<int*>(smem));
+  } else {
+    const int ey = split_exponent(scal[0]), er = split_exponent(scal[1]);
+    inv2 = ldexpf(1.f, -2 * ey);
+    floatx4 accb[CN];
+#pragma unroll
+    for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
+                                       ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
+                                       reinterpret_cast<int*>(smem));
+    rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
+  }
+  if (chunk >= 0) {
+    float* slot = slots + (int64_t)chunk * kW1Slot;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = acc[t][r] * inv2;
+#pragma unroll
+    for (int c = 0; c < CN; ++c) slot[(NT * 4 + c) * 64 + lane] = bt[c];
+    slot[(NT * 4 + CN) * 64 + lane] = (float)npos;
+    return;
+  }
+  wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
+  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
+  w1_finish_and_solve<IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg, X + (int64_t)row * ld,
+                                ld, row, status);
+}
+
+// Launch 2 (W1): heavy rows — fp64 sums of the fp32 chunk partials in a fixed
+// order (+ YtY in fp64 for implicit), one rounding, then the solve.  Entries are
+// reduced 16 at a time (a memory clobber keeps the groups' slot loops apart, so
+// only 16 fp64 sums are live).
+template <bool IMPLICIT>
+__global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
+    const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
+    float* __restrict__ X, int ld, int k, float reg,
+    const double* yty,  // not __restrict__: its loads stay inside their entry group
+    int32_t* __restrict__ status) {
+  constexpr int CN = 8, NT = kW1NT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  const int lane = threadIdx.x & 63;
+  const int h = blockIdx.x;
+  const int row = heavy_rows[h];
+  const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
+  floatx4 A[NT];
+  float bt[CN];
+  float npos_f = 0.f;
+  static_for<(NT * 4 + CN + 1 + 15) / 16>([&](auto gc) {
+    constexpr int g = decltype(gc)::value;
+    double a[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) a[j] = 0.0;
+    for (int s = s0; s < s1; ++s) {
+      const float* sl = slots + (int64_t)s * kW1Slot + lane;
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (16 * g + j < NT * 4 + CN + 1) a[j] += (double)sl[(16 * g + j) * 64];
+    }
+    static_for<16>([&](auto jc) {
+      constexpr int e = 16 * g + decltype(jc)::value;
+      if constexpr (e < NT * 4) {
+        double v = a[decltype(jc)::value];
+        if constexpr (IMPLICIT) {
+          int i, j;
+          tile_ij<8>(FullTiles<8>::l1(e / 4), FullTiles<8>::l2(e / 4), e % 4, i, j);
+          const int hi = i > j ? i : j, lo = i > j ? j : i;
+          v += yty[hi * (hi + 1) / 2 + lo];
+        }
+        A[e / 4][e % 4] = (float)v;
+      } else if constexpr (e < NT * 4 + CN) {
+        bt[e - NT * 4] = (float)a[decltype(jc)::value];
+      } else if constexpr (e == NT * 4 + CN) {
+        npos_f = (float)a[decltype(jc)::value];
+      }
+    });
+    asm volatile("" ::: "memory");
+  });
+  const int64_t n_reg = IMPLICIT ? (int64_t)npos_f : (row_ptr[row + 1] - row_ptr[row]);
+  w1_finish_and_solve<false>(A, 1.f, bt, n_reg, nullptr, smem, k, reg, X + (int64_t)row * ld, ld,
+                             row, status);
 }
 
 // K2b: YtY partial Grams over row chunks of Y (unweighted, identity gather), fp64.
@@ -1637,27 +2095,46 @@ int32_t als_k_pad(int32_t k) { return 16 * cn_for_k(k); }
 
 }  // extern "C"
 
-static size_t slot_doubles(int k) {
+static size_t slot_doubles(int k) {  // partial slot of one heavy-row chunk (solve)
   switch (cn_for_k(k)) {
     case 1: return Cfg<1>::SLOT;
     case 2: return Cfg<2>::SLOT;
     case 4: return Cfg<4>::SLOT;
-    default: return kWgSlot;
+    default: return (size_t)(kW1Slot + 1) / 2;  // W1 stores fp32 partials
   }
+}
+
+static size_t yty_slot_doubles(int k) {  // partial slot of one YtY task
+  return cn_for_k(k) == 8 ? (size_t)kWgSlot : slot_doubles(k);
 }
 
 extern "C" {
 
+static size_t ytyc_bytes(int32_t k) {  // C-layout fp32 YtY table of the W1 path
+  return cn_for_k(k) == 8 ? align_up(sizeof(float) * kW1YtyC) : 0;
+}
+
 static size_t solve_table_bytes(int32_t k, int64_t n_src) {
   return align_up(sizeof(uint32_t) * (size_t)als_k_pad(k) * (size_t)((n_src > 0 ? n_src : 0) + 1));
+}
+
+// Dev switch for A/B timing: ALS_K128_PATH=wg selects the round-1 4-wave workgroup
+// solve for k in (64, 128] (default: W1, one wave per system).
+static bool wg_path() {
+  static const bool v = [] {
+    const char* e = getenv("ALS_K128_PATH");
+    return e && e[0] == 'w' && e[1] == 'g';
+  }();
+  return v;
 }
 
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src) {
   // 256 B of scale words | split table ((n_src + 1) x k_pad words, explicit) |
   // partial slots of the heavy-row chunks.  The first two sit at fixed offsets,
   // so calls over blocks that share Y_src can share one prep (phases).
-  return 256 + solve_table_bytes(k, n_src) +
-         align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
+  const size_t sd = cn_for_k(k) == 8 ? std::max<size_t>(slot_doubles(k), kWgSlot) : slot_doubles(k);
+  return 256 + ytyc_bytes(k) + solve_table_bytes(k, n_src) +
+         align_up(sizeof(double) * sd * (size_t)(n_chunks > 0 ? n_chunks : 0));
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -1693,14 +2170,19 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   // scale words (max |Y_src|, max |rating|), the split table, the partial slots
   unsigned* scal_u = static_cast<unsigned*>(ws);
   const float* scal = reinterpret_cast<const float*>(scal_u);
-  uint32_t* Ysp = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256);
-  double* slots =
-      reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + solve_table_bytes(k, n_src));
+  float* ytyC = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
+  uint32_t* Ysp = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k));
+  double* slots = reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k) +
+                                            solve_table_bytes(k, n_src));
   const int cn = cn_for_k(k);
   const int kp = als_k_pad(k);
   const int zero_row = (int)n_src;
-  if (phases & 4) {  // Y_src prep: max |Y_src|, split table (explicit)
+  if (phases & 4) {  // Y_src prep: max |Y_src|, split table (explicit) / YtY table (W1 implicit)
     ALS_HIP(hipMemsetAsync(scal_u, 0, sizeof(unsigned), st));
+    if (implicit && cn == 8 && !wg_path()) {
+      yty_ctab_kernel<<<1, 64, 0, st>>>(yty_packed, ytyC);
+      ALS_LAUNCH_CHECK();
+    }
     const int64_t ny = n_src * (int64_t)ld;
     if (ny > 0) {
       const int gy = (int)std::min<int64_t>(1024, (ny / 4 + 255) / 256 + 1);
@@ -1755,17 +2237,35 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                       status_dev);                                \
     ALS_LAUNCH_CHECK();                                                                           \
   } while (0)
+#define ALS_SOLVE_W1_LAUNCH(IMP)                                                                  \
+  do {                                                                                            \
+    float* slots_f = reinterpret_cast<float*>(slots);                                             \
+    if (g1)                                                                                       \
+      gram_solve_w1_kernel<IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,    \
+                                                   chunk_end, n_chunks, n_light, Y_src, X_dst,    \
+                                                   ld, k, reg, alpha, ytyC, slots_f, status_dev,  \
+                                                   scal, Ysp, kp, zero_row);                      \
+    ALS_LAUNCH_CHECK();                                                                           \
+    if (g2)                                                                                       \
+      reduce_solve_w1_kernel<IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,      \
+                                                     slots_f, X_dst, ld, k, reg, yty_packed,      \
+                                                     status_dev);                                 \
+    ALS_LAUNCH_CHECK();                                                                           \
+  } while (0)
   if (implicit) {
     if (cn == 1) ALS_SOLVE_LAUNCH(1, true);
     else if (cn == 2) ALS_SOLVE_LAUNCH(2, true);
     else if (cn == 4) ALS_SOLVE_LAUNCH(4, true);
-    else ALS_SOLVE_WG_LAUNCH(true);
+    else if (wg_path()) ALS_SOLVE_WG_LAUNCH(true);
+    else ALS_SOLVE_W1_LAUNCH(true);
   } else {
     if (cn == 1) ALS_SOLVE_LAUNCH(1, false);
     else if (cn == 2) ALS_SOLVE_LAUNCH(2, false);
     else if (cn == 4) ALS_SOLVE_LAUNCH(4, false);
-    else ALS_SOLVE_WG_LAUNCH(false);
+    else if (wg_path()) ALS_SOLVE_WG_LAUNCH(false);
+    else ALS_SOLVE_W1_LAUNCH(false);
   }
+#undef ALS_SOLVE_W1_LAUNCH
 #undef ALS_SOLVE_LAUNCH
 #undef ALS_SOLVE_WG_LAUNCH
   return ALS_OK;
@@ -1773,7 +2273,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
 
 size_t als_yty_workspace_bytes(int64_t n, int32_t k) {
   const int64_t nslots = n > 0 ? (n + kYtyChunk - 1) / kYtyChunk : 1;
-  return align_up(sizeof(double) * slot_doubles(k) * (size_t)nslots) + 256;
+  return align_up(sizeof(double) * yty_slot_doubles(k) * (size_t)nslots) + 256;
 }
 
 int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed_out, void* ws,

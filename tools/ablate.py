@@ -46,10 +46,12 @@ def main():
     L.dev_ablate.argtypes = [ctypes.c_int, P, P, P, P, ctypes.c_int, P, ctypes.c_int, F, F, F, P,
                              ctypes.c_int, F, P, P]
     L.dev_ablate_wg.argtypes = L.dev_ablate.argtypes
+    L.dev_ablate_w1.argtypes = L.dev_ablate.argtypes
     wg = "--wg" in sys.argv
-    k = 128 if wg else 64
-    fn = L.dev_ablate_wg if wg else L.dev_ablate
-    modes = (0, 1, 2) if wg else (0, 1, 2, 5)
+    w1 = "--w1" in sys.argv
+    k = 128 if (wg or w1) else 64
+    fn = L.dev_ablate_w1 if w1 else (L.dev_ablate_wg if wg else L.dev_ablate)
+    modes = (0, 1, 2) if (wg or w1) else (0, 1, 2, 5)
     dev = torch.device("cuda", 0)
     u, i, r = D.synthetic_config("ml25m", device=dev)
     core = E.ALSCore(u, i, r, device=dev)

@@ -60,6 +60,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // Wave-local LDS ordering (lanes of one wave exchanging values through LDS).
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Compiler-only ordering of one wave's LDS accesses: the LDS executes a wave's DS
+// instructions in issue order, so a read issued after a write (any lane) returns
+// the written data without draining lgkmcnt; the compiler inserts the waits for
+// the loaded values where they are used.
+__device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
 
 template <int CN>
 __device__ __forceinline__ void load_dims(const float* __restrict__ p, float (&y)[CN]) {
@@ -1111,31 +1116,66 @@ __device__ __forceinline__ float reduce_lanes16(float v) {
 // update for every lane (the multiplier -B[p][m]/d does not depend on a column's
 // pending scale), and no lane ever forms 1 - 1/d (which cancels for large d).
 // Returns the smallest pivot (> 0 for an SPD block; NaN propagates as "not > 0").
-__device__ __forceinline__ float sweep16(float (&R)[16]) {
+// hook(p) runs after pivot p: the caller interleaves independent matrix-core work
+// there (the asm statements fix the instruction order).
+template <class Hook>
+__device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook) {
   float dmin = 3.0e38f;  // NaN pivots are not seen here: they make the solution NaN
   float dself = 1.f;     // this lane's own pivot (its column's deferred scale is 1/dself)
+  // pivot p's broadcast pivot, reciprocal and multipliers; for p > 0 they are formed
+  // inside pivot p-1, right after row p's update, so their latency (DPP, v_rcp)
+  // hides behind that pivot's remaining row updates
+  float d = bcast16<0>(R[0]);
+  float rd = rcp_t(d);
+  float f = R[0] * rd;
+  float nf = sel_lane16<0>(0.f, -f);
   static_for<16>([&](auto pc) {
     constexpr int p = decltype(pc)::value;
-    const float d = bcast16<p>(R[p]);
     dmin = fminf(dmin, d);
-    const float rd = rcp_t(d);
-    const float f = R[p] * rd;
-    const float nf = sel_lane16<p>(0.f, -f);
     // R[i] += (lane p's R[i]) * nf as ONE v_fmac_f32_dpp per row (the compiler only
     // folds DPP into untied VOP2 ops); s_nop 1 covers the VALU-write -> DPP-read
     // hazard of the previous pivot's last writes.
     asm volatile("s_nop 1" ::: "memory");
-    static_for<16>([&](auto ic) {
+    float dn = 0.f, rdn = 0.f, fn = 0.f, nfn = 0.f;
+    auto row = [&](auto ic) {
       constexpr int i = decltype(ic)::value;
       if constexpr (i != p) fmac_bcast16<p>(R[i], nf);
+      if constexpr (i == p + 1) {  // row p+1 is final for pivot p+1: start it now
+        asm volatile("s_nop 1" ::: "memory");
+        dn = bcast16<p + 1>(R[p + 1]);
+        rdn = rcp_t(dn);
+        fn = R[p + 1] * rdn;
+        nfn = sel_lane16<p + 1>(0.f, -fn);
+      }
+    };
+    // row p+1 first, then the others
+    if constexpr (p + 1 < 16) row(std::integral_constant<int, p + 1>{});
+    static_for<16>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr (i != p + 1) row(ic);
     });
     R[p] = sel_lane16<p>(-1.f, f);
     dself = sel_lane16<p>(d, dself);
+    hook(pc);
+    d = dn; rd = rdn; f = fn; nf = nfn;
   });
   const float s = rcp_t(dself);
 #pragma unroll
   for (int i = 0; i < 16; ++i) R[i] *= s;
   return dmin;
+}
+
+// Schur tiles of step K, I-major: u = 0 is (K+1, K+1), the next pivot block.
+__host__ __device__ constexpr int schur_n(int K) { return (7 - K) * (8 - K) / 2; }
+__host__ __device__ constexpr int schur_I(int K, int u) {
+  int I = K + 1;
+  while (u >= 8 - I) { u -= 8 - I; ++I; }
+  return I;
+}
+__host__ __device__ constexpr int schur_J(int K, int u) {
+  int I = K + 1;
+  while (u >= 8 - I) { u -= 8 - I; ++I; }
+  return I + u;
 }
 
 template <int NT>
@@ -1153,19 +1193,21 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
   // block J becomes the pivot block): start with the full b_J in row group 0
 #pragma unroll
   for (int c = 1; c < NB; ++c) bcol[c] = q == 0 ? bcol[c] : 0.f;
-  static_for<NB>([&](auto Kc) {
+  // Sweep block K from its tile (C layout -> column per lane through LDS), running
+  // `hook` between pivots; then Gm_K (C layout) and b_K (row layout).
+  floatx4 Gm, bk;
+  auto pivot_block = [&](auto Kc, auto&& hook) {
     constexpr int K = decltype(Kc)::value;
-    // (1) diagonal block: C layout -> column per lane (LDS), sweep, -> C layout
     *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile(K, K)];
-    wave_lds_sync();
+    wave_lds_order();
     float R[16];
 #pragma unroll
     for (int c4 = 0; c4 < 4; ++c4) {
       const floatx4 v = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * c4);
       R[4 * c4] = v[0]; R[4 * c4 + 1] = v[1]; R[4 * c4 + 2] = v[2]; R[4 * c4 + 3] = v[3];
     }
-    dmin = fminf(dmin, sweep16(R));
-    wave_lds_sync();
+    dmin = fminf(dmin, sweep16(R, hook));
+    wave_lds_order();
     const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
     if (q == 0) {
 #pragma unroll
@@ -1174,15 +1216,29 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
             floatx4{R[4 * c4], R[4 * c4 + 1], R[4 * c4 + 2], R[4 * c4 + 3]};
       vec[m] = bK;
     }
-    wave_lds_sync();
-    const floatx4 Gm = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * q);  // C layout
-    const floatx4 bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);          // row layout
-    wave_lds_sync();
+    wave_lds_order();
+    Gm = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * q);  // C layout
+    bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);           // row layout
+    wave_lds_order();
+  };
+  auto schur = [&](auto Kc, auto uc, const floatx4 (&Pm)[NB]) {
+    constexpr int K = decltype(Kc)::value, u = decltype(uc)::value;
+    constexpr int I = schur_I(K, u), J = schur_J(K, u);
+    floatx4 acc = A[w1_tile(I, J)];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[w1_tile(K, I)][s4], Pm[J - K - 1][s4], acc, 0,
+                                                  0, 0);
+    A[w1_tile(I, J)] = acc;
+  };
+  pivot_block(std::integral_constant<int, 0>{}, [](auto) {});
+  static_for<NB>([&](auto Kc) {
+    constexpr int K = decltype(Kc)::value;
     // z_K = -Gm b_K  (Gm symmetric: (Gm b)[i] = sum_k Gm[k][i] b[k])
     zcol[K] = -reduce_rows4(Gm[0] * bk[0] + Gm[1] * bk[1] + Gm[2] * bk[2] + Gm[3] * bk[3]);
     if constexpr (K + 1 < NB) {
-      // (2) Pm_J = Gm B_KJ;  b_J += Pm_J^T b_K
-      floatx4 Pm[NB - 1 - K];
+      // Pm_J = Gm B_KJ;  b_J += Pm_J^T b_K (per-row-group partials)
+      floatx4 Pm[NB];
       static_for<NB - 1 - K>([&](auto jc) {
         constexpr int J = K + 1 + decltype(jc)::value;
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1190,27 +1246,23 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
         for (int s4 = 0; s4 < 4; ++s4)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Gm[s4], A[w1_tile(K, J)][s4], acc, 0, 0, 0);
         Pm[decltype(jc)::value] = acc;
-        // b_J += Pm_J^T b_K, kept as per-row-group partials until J is the pivot block
         bcol[J] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
       });
-      // (3) Schur complement B_IJ += B_KI^T Pm_J, K < I <= J
-      static_for<NB - 1 - K>([&](auto ic) {
-        constexpr int I = K + 1 + decltype(ic)::value;
-        static_for<NB - I>([&](auto jc) {
-          constexpr int J = I + decltype(jc)::value;
-          floatx4 acc = A[w1_tile(I, J)];
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[w1_tile(K, I)][s4], Pm[J - K - 1][s4],
-                                                        acc, 0, 0, 0);
-          A[w1_tile(I, J)] = acc;
-        });
-      });
-      // (4) Pm of block row K -> LDS for the back substitution (lane-private slots)
+      // Pm of block row K -> LDS for the back substitution (lane-private slots)
       static_for<NB - 1 - K>([&](auto jc) {
         constexpr int J = K + 1 + decltype(jc)::value;
         *reinterpret_cast<floatx4*>(lds + W1Lds::PM + (w1_tile(K, J) - (K + 1)) * 256 + 4 * lane) =
             Pm[decltype(jc)::value];
+      });
+      // the next pivot block's Schur update first, then its sweep with the rest of
+      // step K's Schur updates (independent of it) issued between the pivots
+      schur(Kc, std::integral_constant<int, 0>{}, Pm);
+      pivot_block(std::integral_constant<int, K + 1>{}, [&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        static_for<schur_n(K) - 1>([&](auto vc) {
+          constexpr int u = 1 + decltype(vc)::value;
+          if constexpr ((u - 1) % 16 == p) schur(Kc, std::integral_constant<int, u>{}, Pm);
+        });
       });
     }
   });
@@ -1230,9 +1282,9 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
 #pragma unroll
     for (int r = 0; r < 4; ++r) pr[r] = reduce_lanes16(pr[r]);  // rows 4q+r of Pm x
     if (m == 0) *reinterpret_cast<floatx4*>(vec + 4 * q) = floatx4{pr[0], pr[1], pr[2], pr[3]};
-    wave_lds_sync();
+    wave_lds_order();
     xcol[K] = zcol[K] + vec[m];
-    wave_lds_sync();
+    wave_lds_order();
   });
   // a NaN pivot (or overflow) leaves a non-finite solution
   bool fin = true;

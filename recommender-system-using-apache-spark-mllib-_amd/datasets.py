@@ -96,6 +96,7 @@ CONFIGS = {
     "ml1m_lab4": (6040, 3706, 292716, False, 0),        # SURVEY 0a (script-as-written)
     "ml_latest_small": (610, 9724, 100836, True, 0),    # SURVEY 0b (BASELINE configs[0])
     "ml25m": (162541, 59047, 25000095, True, 1),         # BASELINE configs[1] / [2]
+    "big1b": (10_000_000, 1_000_000, 1_000_000_000, True, 2),  # BASELINE configs[3] / [4]
 }
 
 
@@ -191,3 +192,113 @@ def synthetic_config(name: str, device="cuda", scale_users: int = 1, shard: int 
     n_u, n_i, nnz, half, seed = CONFIGS[name]
     return synthetic(n_u, n_i, nnz, seed=seed, half_stars=half, device=device,
                      user_offset=shard * n_u)
+
+
+# ---------------------------------------------------------------- 1B-rating power law
+def synthetic_blocked(n_users: int, n_items: int, nnz: int, seed: int = 2, half_stars: bool = True,
+                      device="cuda", user_begin: int = 0, user_end: int = None,
+                      block_ratings: int = 1 << 26, k_true: int = 16):
+    """BASELINE configs[3]: the planted model of `synthetic` at 1e9-rating scale,
+    generated on the device in user blocks (never the whole key set at once).
+
+    Users [user_begin, user_end) of one global dataset are produced, so ranks of a
+    sharded job generate disjoint user ranges whose union is exactly the
+    single-process dataset (every quantity is derived from `seed` and the global
+    user index).  Degrees: log-normal (min 20) scaled to `nnz` over ALL users;
+    items: Zipf(0.9) popularity capped at half the users (SURVEY.md §8d caps the
+    head item at n_users).  Exactly sum(degree) distinct (user, item) pairs per
+    user range; returns (users int32, items int32, ratings f32) on `device`."""
+    dev = torch.device(device)
+    user_end = n_users if user_end is None else user_end
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed * 1000003)
+    deg = torch.exp(torch.randn(n_users, generator=g, dtype=torch.float64) + 4.2)
+    deg = 20 + deg * max(nnz - 20 * n_users, 0) / deg.sum()
+    deg = deg.clamp(max=n_items * 0.5)
+    d = torch.floor(deg).long()
+    short = nnz - int(d.sum())
+    if short > 0:  # distribute the rounding remainder by the fractional parts
+        frac = deg - d
+        cf = torch.cumsum(frac, 0)
+        add = torch.searchsorted(cf / cf[-1], torch.rand(short, generator=g, dtype=torch.float64))
+        d += torch.bincount(add.clamp(max=n_users - 1), minlength=n_users)
+    del deg
+    pop = _zipf_probs(n_items, 0.9, 0.5 * n_users / nnz)
+    cdf_i = torch.cumsum(pop, 0)
+    cdf_i = (cdf_i / cdf_i[-1]).to(torch.float32).to(dev)
+    gi = torch.Generator(device="cpu")
+    gi.manual_seed(seed * 15485863)
+    perm_items = torch.randperm(n_items, generator=gi).to(dev)
+    gv = torch.Generator(device=dev)
+    gv.manual_seed(seed * 104729)
+    vs = torch.randn((n_items, k_true), generator=gv, device=dev) * 0.35
+    out_u, out_i, out_r = [], [], []
+    # GLOBAL blocks of consecutive users with about block_ratings ratings each (a
+    # block's draws depend only on its global start, so shards reproduce the
+    # single-process data); the blocks overlapping [user_begin, user_end) are made
+    # whole and filtered to the range
+    cum = torch.cumsum(d, 0)
+    n_blk = max(1, -(-int(cum[-1]) // block_ratings))
+    targets = torch.arange(1, n_blk, dtype=torch.int64) * block_ratings
+    bounds = [0] + [int(c) for c in torch.searchsorted(cum, targets, right=True)] + [n_users]
+    for b0, b1 in zip(bounds[:-1], bounds[1:]):
+        if b1 <= b0 or b1 <= user_begin or b0 >= user_end:
+            continue
+        ub = b0
+        dblk = d[b0:b1].to(dev)
+        need = int(dblk.sum())
+        gb = torch.Generator(device=dev)
+        gb.manual_seed(seed * 7919 + ub)  # per block of GLOBAL users: shard-independent
+        users = torch.repeat_interleave(torch.arange(b1 - b0, device=dev), dblk)
+        keys = torch.empty(0, dtype=torch.int64, device=dev)
+        want = users
+        for _ in range(64):
+            x = torch.rand(want.numel(), generator=gb, device=dev)
+            it = torch.searchsorted(cdf_i, x).clamp(max=n_items - 1)
+            keys = torch.unique(torch.cat([keys, want * n_items + it]))
+            # per-user counts vs degrees: users still short get more draws
+            have = torch.bincount(keys // n_items, minlength=b1 - b0)
+            miss = (dblk - have).clamp(min=0)
+            if int(miss.sum()) == 0:
+                break
+            want = torch.repeat_interleave(torch.arange(b1 - b0, device=dev), miss * 2 + 2)
+        else:
+            raise RuntimeError("synthetic_blocked: could not reach the user degrees")
+        # keep exactly deg(u) items per user: random rank within the user
+        ku = keys // n_items
+        pri = torch.rand(keys.numel(), generator=gb, device=dev)
+        order = torch.argsort(ku.double() + pri.double() * 0.5)  # users ascending, random within
+        keys = keys[order]
+        ku = ku[order]
+        start = torch.cumsum(torch.bincount(ku, minlength=b1 - b0), 0) - torch.bincount(
+            ku, minlength=b1 - b0)
+        rank_in_user = torch.arange(keys.numel(), device=dev) - start[ku]
+        keys = keys[rank_in_user < dblk[ku]]
+        assert keys.numel() == need
+        uu = keys // n_items
+        ii = perm_items[keys % n_items]
+        us = torch.randn((b1 - b0, k_true), generator=gb, device=dev) * 0.35
+        dot = (us[uu] * vs[ii]).sum(1)
+        x = 3.6 + dot + 0.8 * torch.randn(need, generator=gb, device=dev)
+        r = (torch.round(x * 2) / 2).clamp(0.5, 5.0) if half_stars else torch.round(x).clamp(1.0, 5.0)
+        sh = torch.randperm(need, generator=gb, device=dev)  # input order is not sorted
+        ug = uu[sh] + ub
+        keep = (ug >= user_begin) & (ug < user_end)
+        out_u.append(ug[keep].to(torch.int32))
+        out_i.append(ii[sh][keep].to(torch.int32))
+        out_r.append(r[sh][keep].to(torch.float32))
+        del keys, ku, users, uu, ii, us, dot, x, r, sh, order, pri, rank_in_user
+    if not out_u:
+        z = torch.empty(0, dtype=torch.int32, device=dev)
+        return z, z, z.float()
+    return torch.cat(out_u), torch.cat(out_i), torch.cat(out_r)
+
+
+def big_config(name: str = "big1b", device="cuda", rank: int = 0, world: int = 1):
+    """configs[3] data for process `rank` of `world` (strong scaling: the user range is
+    split in `world` contiguous parts of one global dataset)."""
+    n_u, n_i, nnz, half, seed = CONFIGS[name]
+    b = n_u * rank // world
+    e = n_u * (rank + 1) // world
+    return synthetic_blocked(n_u, n_i, nnz, seed=seed, half_stars=half, device=device,
+                             user_begin=b, user_end=e)

@@ -115,3 +115,26 @@ def test_synthetic_generator_shape_cpu():
     assert int(i.max()) < 200 and int(u.max()) < 300
     u2, i2, r2 = datasets.synthetic(300, 200, 6000, seed=3, device="cpu")
     assert (u == u2).all() and (i == i2).all() and (r == r2).all()
+
+
+def test_blocked_generator_shards_reproduce_single_process():
+    """configs[3]'s generator: exact nnz, no duplicate pairs, min user degree 20, and
+    the union of the user-range shards equals the single-process dataset (strong
+    scaling generates one global dataset)."""
+    import numpy as np
+    from als_mi355x import datasets as D
+    kw = dict(n_users=6000, n_items=2000, nnz=300_000, seed=3, device="cpu",
+              block_ratings=1 << 15)
+    u, i, r = D.synthetic_blocked(**kw)
+    assert u.numel() == 300_000
+    keys = u.long() * 2000 + i.long()
+    assert keys.unique().numel() == keys.numel()
+    assert np.bincount(u.numpy()).min() >= 20
+    assert float(r.min()) >= 0.5 and float(r.max()) <= 5.0
+    parts = [D.synthetic_blocked(user_begin=6000 * w // 4, user_end=6000 * (w + 1) // 4, **kw)
+             for w in range(4)]
+    a = np.stack([u.numpy(), i.numpy(), r.numpy().view(np.int32)], 1)
+    b = np.concatenate([np.stack([x.numpy(), y.numpy(), z.numpy().view(np.int32)], 1)
+                        for x, y, z in parts])
+    np.testing.assert_array_equal(a[np.lexsort((a[:, 1], a[:, 0]))],
+                                  b[np.lexsort((b[:, 1], b[:, 0]))])

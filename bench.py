@@ -1,24 +1,33 @@
 #!/usr/bin/env python3
-"""ALS hot-path benchmark — BASELINE.json metric "ratings/sec per ALS iteration (rank 64)".
+"""ALS hot-path benchmark — BASELINE.json metric
+"ratings/sec per ALS iteration (rank 64) at 1/2/4/8 GPUs; top-10 recs/sec".
 
-Workload (BASELINE.json configs[1]): MovieLens-25M-shaped synthetic ratings,
-162,541 users x 59,047 items, 25,000,095 ratings, explicit ALS, rank 64,
-regParam 0.1 — generated on the device (seeded planted model).
-A "step" is one full ALS iteration exactly as Spark runs it: the item
-half-sweep (normal equations + Cholesky for every item from the user factors)
-then the user half-sweep, plus the factor all-gathers when N > 1.
+Primary line (`value`), every N: BASELINE.json configs[1], MovieLens-25M-shaped
+synthetic ratings (162,541 users x 59,047 items, 25,000,095 ratings), explicit
+ALS, rank 64, regParam 0.1, generated on the device (seeded planted model,
+SURVEY.md §8d).  A "step" is one full ALS iteration exactly as Spark runs it:
+the item half-sweep (normal equations + Cholesky-equivalent solve for every
+item from the user factors) then the user half-sweep, plus the factor
+all-gathers when N > 1.  N > 1 is weak scaling of this workload: rank r owns
+its own 162,541-user shard of one global dataset (same items); value = all
+ratings / max-over-ranks time.
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): weak scaling —
-every rank generates its own 162,541-user shard of one global dataset (same
-59,047 items), ratings are routed once to their user-row and item-row owners
-(all_to_all), and each half-sweep ends with an RCCL all_gather of the updated
-factor half.  value = total ratings of all ranks / max-over-ranks time.
+Secondary objects on the same line (BASELINE configs[3] and [4], the
+north-star scaling workload; `--no-big` skips them):
+  configs3: 1e9-rating power-law synthetic, 10M users x 1M items, rank 128,
+            explicit — STRONG scaling: the one global dataset is split over the N
+            ranks by user range (each rank generates its range; ShardedALS routes
+            ratings to row owners, RCCL all-gathers the factor halves), value =
+            1e9 / iteration time.  N = 1 uses the single-GPU engine.
+  configs4: recommendForAllUsers top-10 and top-100 on those rank-128 factors,
+            over a user sample (262,144 users, split over the ranks; items all
+            1M), recs/s = sampled users / time.
 
-Also reported: `roofline` of the dominant kernel (gram_solve_kernel<4,false>,
-timed with HIP events on its own stream), `cpu_baseline` (the C port of
-Spark's per-row dspr + dppsv arithmetic, oracle/als_oracle.c, on the host
-cores, bounded sample), top-10 recs/s (recommendForAllUsers(10), N = 1 only)
-and the training RMSE.
+Also: `roofline` of the dominant kernel (timed with HIP events on its own
+stream; algorithmic bytes and MFMA flops per launch, PMC traffic and
+utilisation from the committed rocprofv3 summary), `topk_roofline`,
+`cpu_baseline` (the C port of Spark's per-row dspr + dppsv arithmetic,
+oracle/als_oracle.c, on the host cores, bounded sample).
 """
 from __future__ import annotations
 
@@ -40,23 +49,45 @@ als = _pkgload.load()
 from als_mi355x import datasets as D  # noqa: E402
 from als_mi355x import engine as E  # noqa: E402
 
-PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 matrix, spec
+# MI355X_MICROARCH.md (dense, no sparsity): fp32 matrix/vector 157.3 TF, f16 matrix 2.5 PF
+PEAK_FP32_TFLOPS = 157.3
+PEAK_F16_MFMA_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_summary.json")
+BIG_TOPK_SAMPLE = 262144
 
 
 def dominant_kernel(k: int, implicit: bool) -> str:
     imp = "true" if implicit else "false"
     if k > 64:
-        return f"gram_solve_wg_kernel<{imp}>"
+        return f"gram_solve_w1_kernel<{imp}>"
     cn = 1 if k <= 16 else (2 if k <= 32 else 4)
     return f"gram_solve_kernel<{cn},{imp}>"
 
 
-def gram_flops(nnz: int, n_solved: int, k: int) -> float:
-    """Algorithmic FLOPs of launch 1 of a half-sweep: symmetric Gram k(k+1)/2 FMAs and the
-    rhs k FMAs per rating, plus Cholesky (k^3/3) + two triangular solves (2k^2) per row
-    solved in the same launch."""
+def kp_of(k: int) -> int:
+    return 16 if k <= 16 else (32 if k <= 32 else (64 if k <= 64 else 128))
+
+
+def algorithmic_flops(nnz: int, n_solved: int, k: int) -> float:
+    """fp32-grade FLOPs of launch 1 of a half-sweep: symmetric Gram
+    k(k+1) and rhs 2k per rating, Cholesky k^3/3 + two triangular solves 2k^2 per row."""
     return nnz * (k * (k + 1) + 2 * k) + n_solved * (k ** 3 / 3 + 2 * k ** 2)
+
+
+def mfma_issued_flops(nnz: int, n_solved: int, k: int, implicit: bool) -> float:
+    """Matrix-core FLOPs the kernel actually issues per launch (what the MFMA pipes do):
+    Gram: upper 16x16 tiles x 3 f16 MFMAs (split hi/lo) per 32 ratings (+ 2 rhs MFMAs
+    per dims-block, explicit); solve: fp32 16x16x4 trailing / block-row products."""
+    cn = kp_of(k) // 16
+    nt = cn * (cn + 1) // 2
+    per32 = (3 * nt + (0 if implicit else 2 * cn)) * 16 * 16 * 32 * 2
+    gram = nnz / 32.0 * per32
+    if cn == 8:   # W1: 28 Pm + 84 Schur tile products, 4 x 16x16x4 each
+        solve = (28 + 84) * 4 * 16 * 16 * 4 * 2
+    else:         # panel LDL^T: trailing tile updates, 4 x 16x16x4 each
+        solve = sum((cn - 1 - K) * (cn - K) // 2 for K in range(cn)) * 4 * 16 * 16 * 4 * 2
+    return gram + n_solved * solve
 
 
 def gather_bytes(nnz: int, n_rows: int, k: int) -> float:
@@ -67,16 +98,81 @@ def gather_bytes(nnz: int, n_rows: int, k: int) -> float:
 
 
 def load_pmc(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (tools/profile.sh -> tools/pmc_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    """Per-launch rocprofv3 counters of `kernel` from the committed summary
+    (tools/pmc_fold.py over profiles/r02_*), or None."""
     try:
-        with open(path) as f:
+        with open(PMC_FILE) as f:
             d = json.load(f)
-        ent = d.get(kernel.replace(" ", ""))
-        return None if ent is None else ent.get("hbm_bytes_per_launch")
+        return d.get("kernels", {}).get(kernel.replace(" ", ""))
     except Exception:
         return None
+
+
+def roofline(kernel: str, launch_ms: dict, nnz_rows: list, k: int, implicit: bool):
+    """launch_ms: {"item": ms, "user": ms} averages of launch 1 of each half-sweep."""
+    launch_s = sum(launch_ms.values()) * 1e-3
+    n_launch = len(launch_ms)
+    b = sum(gather_bytes(nz, rows, k) for nz, rows in nnz_rows)
+    f = sum(algorithmic_flops(nz, rows, k) for nz, rows in nnz_rows)
+    fm = sum(mfma_issued_flops(nz, rows, k, implicit) for nz, rows in nnz_rows)
+    hbm = b / launch_s / 1e9
+    mfma = fm / launch_s / 1e12
+    pmc = load_pmc(kernel)
+    out = {
+        "kernel": kernel,
+        "avg_launch_us": 1e6 * launch_s / n_launch,
+        "launch_ms": launch_ms,
+        "algorithmic_bytes_per_launch": b / n_launch,
+        "hbm_view": {"achieved_gbs": hbm, "peak_gbs": PEAK_HBM_GBS, "frac": hbm / PEAK_HBM_GBS},
+        "mfma_view": {"issued_flops_per_launch": fm / n_launch, "achieved_tflops": mfma,
+                      "peak_tflops": PEAK_F16_MFMA_TFLOPS,
+                      "frac": mfma / PEAK_F16_MFMA_TFLOPS,
+                      "note": "f16 matrix-core flops issued (split-f16 Gram: 3 MFMAs per "
+                              "fp32-grade product) + fp32 16x16x4 solve flops"},
+        "fp32_grade_view": {"algorithmic_flops_per_launch": f / n_launch,
+                            "achieved_tflops": f / launch_s / 1e12,
+                            "peak_tflops": PEAK_FP32_TFLOPS},
+    }
+    traffic = None
+    if pmc:
+        t = pmc.get("fetch_bytes_x2", 0.0) + pmc.get("write_bytes", 0.0)
+        traffic = t if t > 0 else None
+        out["pmc"] = {k_: pmc[k_] for k_ in ("mfma_busy_frac", "valu_busy_frac", "fetch_bytes_x2",
+                                             "write_bytes", "pmc_run_avg_ns", "eff_clock_ghz")
+                      if k_ in pmc}
+        out["pmc"]["source"] = os.path.relpath(PMC_FILE, ROOT)
+        busy = {"valu": pmc.get("valu_busy_frac"), "mfma": pmc.get("mfma_busy_frac"),
+                "hbm": (traffic / (1e-6 * out["avg_launch_us"]) / 1e9 / PEAK_HBM_GBS)
+                if traffic else None}
+        busy = {k_: v for k_, v in busy.items() if v is not None}
+        if busy:
+            out["limiter"] = max(busy, key=busy.get)
+            out["limiter_fracs"] = busy
+    # contract: bound in {hbm, mfma}; the larger of the two live fractions
+    bound = "hbm" if out["hbm_view"]["frac"] >= out["mfma_view"]["frac"] else "mfma"
+    view = out["hbm_view"] if bound == "hbm" else out["mfma_view"]
+    out.update({"bound": bound,
+                "achieved": view["achieved_gbs"] if bound == "hbm" else view["achieved_tflops"],
+                "peak": PEAK_HBM_GBS if bound == "hbm" else PEAK_F16_MFMA_TFLOPS,
+                "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
+                "frac": view["frac"], "traffic": traffic})
+    return out
+
+
+def topk_roofline(n_q: int, n_v: int, k: int, ms: float, top: int):
+    useful = 2.0 * n_q * n_v * k
+    issued = 3.0 * 2.0 * n_q * n_v * kp_of(k)
+    s = ms * 1e-3
+    out = {"kernel": "topk_split_kernel", "top": top, "n_q": n_q, "n_v": n_v, "rank": k,
+           "ms": ms, "recs_per_s": n_q / s,
+           "useful_fp32_grade_tflops": useful / s / 1e12,
+           "issued_f16_mfma_tflops": issued / s / 1e12,
+           "mfma_frac": issued / s / 1e12 / PEAK_F16_MFMA_TFLOPS,
+           "bound": "mfma", "unit": "TFLOP/s"}
+    pmc = load_pmc("topk_split_kernel")
+    if pmc:
+        out["pmc_mfma_busy_frac"] = pmc.get("mfma_busy_frac")
+    return out
 
 
 def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.0,
@@ -116,10 +212,64 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
                       + "; full-iteration time extrapolated as sum over sides of nnz/rate"}
 
 
+def _timed_topk(Q, n_q, V, n_v, k, top):
+    E.topk_rows(Q, n_q, V, n_v, k, top)  # warm (workspace, split table)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    E.topk_rows(Q, n_q, V, n_v, k, top)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1)
+
+
+def big_single(args, dev):
+    """configs[3] (N = 1) and configs[4] on its factors."""
+    k = 128
+    t0 = time.perf_counter()
+    u, i, r = D.big_config("big1b", device=dev)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    core = E.ALSCore(u, i, r, device=dev)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    del u, i, r
+    torch.cuda.empty_cache()
+    core.init_factors(k, seed=5)
+    core.status.zero_()
+    steps = max(1, min(args.steps, args.big_steps))
+    core.iterate(args.reg)  # warmup
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        core.iterate(args.reg)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    core.check_status()
+    res = {"workload": "big1b explicit ALS rank 128 (BASELINE configs[3]), 1 GPU",
+           "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz, "rank": k,
+           "ratings_per_s": core.nnz / dt, "ms_per_iter": 1e3 * dt, "steps": steps,
+           "warmup": 1, "datagen_s": t_gen, "build_s": t_build, "scaling": "strong",
+           "n_gpus": 1}
+    s = min(BIG_TOPK_SAMPLE, core.n_users)
+    Q = core.U[:s].contiguous()
+    c4 = {"workload": f"recommendForAllUsers on configs[3] factors (BASELINE configs[4]); "
+                      f"sample: first {s} users (dense order) x all {core.n_items} items",
+          "rank": k}
+    for top in (10, 100):
+        ms = _timed_topk(Q, s, core.V, core.n_items, k, top)
+        c4[f"top{top}_recs_per_s"] = s / (ms * 1e-3)
+        c4[f"top{top}_ms"] = ms
+        c4[f"top{top}_roofline"] = topk_roofline(s, core.n_items, k, ms, top)
+    del core
+    torch.cuda.empty_cache()
+    return res, c4
+
+
 def run_single(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    n_u, n_i, nnz_cfg, _, _ = D.CONFIGS[args.config]
     t0 = time.perf_counter()
     u, i, r = D.synthetic_config(args.config, device=dev)
     torch.cuda.synchronize()
@@ -135,7 +285,6 @@ def run_single(args):
     core.init_factors(k, seed=5)
     core.status.zero_()
     ib, ub = core.item_block, core.user_block
-
     imp, alpha = args.implicit, args.alpha
 
     def iteration(evs=None):
@@ -171,29 +320,14 @@ def run_single(args):
     ms_per_step = 1000.0 * t_total / args.steps
     value = core.nnz / (t_total / args.steps)
 
-    # roofline of the dominant kernel (launch 1 of each half-sweep)
+    # roofline of the dominant kernel (launch 1 of each half-sweep, HIP events on its stream)
     item_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     user_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    f_item = gram_flops(ib.nnz, ib.n_light, k)
-    f_user = gram_flops(ub.nnz, ub.n_light, k)
-    b_item = gather_bytes(ib.nnz, ib.n_light, k)
-    b_user = gather_bytes(ub.nnz, ub.n_light, k)
-    launch_s = (item_ms + user_ms) * 1e-3
-    achieved = (b_item + b_user) / launch_s / 1e9
-    tflops = (f_item + f_user) / launch_s / 1e12
-    avg_launch_us = 1000.0 * (item_ms + user_ms) / 2
-    dominant = dominant_kernel(k, imp)
-    traffic = load_pmc(dominant)
+    roof = roofline(dominant_kernel(k, imp), {"item": item_ms, "user": user_ms},
+                    [(ib.nnz, ib.n_light), (ub.nnz, ub.n_light)], k, imp)
 
-    # top-10 recommendations for all users (K5), timed with events after one warm run
-    core.recommend_users(10)
-    torch.cuda.synchronize()
-    t0e, t1e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0e.record()
-    core.recommend_users(10)
-    t1e.record()
-    torch.cuda.synchronize()
-    topk_ms = t0e.elapsed_time(t1e)
+    # top-10 recommendations for all users (K5)
+    topk_ms = _timed_topk(core.U, core.n_users, core.V, core.n_items, k, 10)
     mode = f"implicit alpha={alpha:g}" if imp else "explicit"
     cfg_idx = 2 if (imp and k == 128) else 1
     out = {
@@ -214,19 +348,10 @@ def run_single(args):
                    "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz,
                    "rank": k, "regParam": args.reg, "implicitPrefs": imp, "alpha": alpha,
                    "parallelism": "dp1"},
-        "roofline": {"bound": "hbm", "kernel": dominant,
-                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                     "avg_launch_us": avg_launch_us,
-                     "algorithmic_bytes_per_launch": (b_item + b_user) / 2,
-                     "launch_ms": {"item": item_ms, "user": user_ms},
-                     "flops_view": {"algorithmic_flops_per_launch": (f_item + f_user) / 2,
-                                    "achieved_tflops": tflops,
-                                    "note": "fp32-grade Gram on f16 MFMA (3 products per "
-                                            "fp32 product, k<=64); peak f16 dense 2500 TF, "
-                                            "fp32 157.3 TF"}},
+        "roofline": roof,
         "topk10_recs_per_s": core.n_users / (topk_ms * 1e-3),
         "topk10_ms": topk_ms,
+        "topk_roofline": topk_roofline(core.n_users, core.n_items, k, topk_ms, 10),
         "csr_build_ms": build_ms,
         "datagen_s": t_gen,
         "schedule": {"item": [ib.n_light, ib.n_heavy, ib.n_chunks],
@@ -239,6 +364,13 @@ def run_single(args):
         out["cpu_baseline"] = cpu_baseline(core, k, args.reg, args.cpu_budget, imp, alpha)
     else:
         out["cpu_baseline"] = None
+    del core, ib, ub
+    torch.cuda.empty_cache()
+    if args.big:
+        try:
+            out["configs3"], out["configs4"] = big_single(args, dev)
+        except Exception as e:  # the primary line must still print
+            out["configs3"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     print(json.dumps(out), flush=True)
 
 
@@ -247,7 +379,69 @@ def _train_triples(core):
     ub = core.user_block
     deg = ub.row_ptr[1:] - ub.row_ptr[:-1]
     rows = torch.repeat_interleave(torch.arange(ub.n_rows, device=deg.device), deg)
-    return core.uidx.uniq[rows], core.iidx.uniq[ub.col.long()], ub.val
+    return core.uidx.ids()[rows], core.iidx.ids()[ub.col.long()], ub.val
+
+
+def _timed_iterations(sh, reg, warmup, steps, dev):
+    for _ in range(warmup):
+        sh.iterate(reg)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sh.iterate(reg)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return float(dt)
+
+
+def big_distributed(args, dev, rank, world):
+    """configs[3] strong scaling over the ranks + configs[4] on the sharded factors."""
+    from als_mi355x.distributed import ShardedALS
+    k = 128
+    t0 = time.perf_counter()
+    u, i, r = D.big_config("big1b", device=dev, rank=rank, world=world)
+    torch.cuda.synchronize()
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    sh = ShardedALS(u, i, r, device=dev, chunks=args.chunks)
+    torch.cuda.synchronize()
+    t_build = time.perf_counter() - t0
+    del u, i, r
+    torch.cuda.empty_cache()
+    sh.init_factors(k, seed=5)
+    steps = max(1, min(args.steps, args.big_steps))
+    t = _timed_iterations(sh, args.reg, 1, steps, dev)
+    sh.check_status()
+    res = {"workload": f"big1b explicit ALS rank 128 (BASELINE configs[3]), {world} GPUs, "
+                       "users split by range, RCCL factor all-gather",
+           "n_users": sh.n_users, "n_items": sh.n_items, "nnz": sh.nnz, "rank": k,
+           "ratings_per_s": sh.nnz / (t / steps), "ms_per_iter": 1e3 * t / steps,
+           "steps": steps, "warmup": 1, "datagen_s": t_gen, "build_s": t_build,
+           "scaling": "strong", "n_gpus": world, "chunks": sh.users.chunks}
+    # configs[4]: each rank scores its share of the user sample against the replicated V
+    s_loc = min(BIG_TOPK_SAMPLE // world, sh.users.chunk_rows(rank, 0))
+    Vd = sh._dense(False)
+    Q = sh.U_loc[0, :s_loc].contiguous()
+    c4 = {"workload": f"recommendForAllUsers on configs[3] factors (BASELINE configs[4]); "
+                      f"sample: {s_loc} users per rank x {world} ranks x all {sh.n_items} items",
+          "rank": k}
+    for top in (10, 100):
+        E.topk_rows(Q, s_loc, Vd, sh.n_items, k, top)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        E.topk_rows(Q, s_loc, Vd, sh.n_items, k, top)
+        torch.cuda.synchronize()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        c4[f"top{top}_recs_per_s"] = s_loc * world / float(dt)
+        c4[f"top{top}_ms"] = 1e3 * float(dt)
+    return res, c4
 
 
 def run_distributed(args):
@@ -265,20 +459,8 @@ def run_distributed(args):
     del u, i, r
     k = args.rank
     sh.init_factors(k, seed=5)
-    for _ in range(args.warmup):
-        sh.iterate(args.reg)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sh.iterate(args.reg)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    t_total = float(dt)
+    t_total = _timed_iterations(sh, args.reg, args.warmup, args.steps, dev)
+    out = None
     if rank == 0:
         out = {
             "metric": "ratings/sec per ALS iteration (rank 64)",
@@ -300,6 +482,17 @@ def run_distributed(args):
             "roofline": None,
             "cpu_baseline": None,
         }
+    del sh
+    torch.cuda.empty_cache()
+    if args.big:
+        try:
+            c3, c4 = big_distributed(args, dev, rank, world)
+            if rank == 0:
+                out["configs3"], out["configs4"] = c3, c4
+        except Exception as e:
+            if rank == 0:
+                out["configs3"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
 
@@ -317,8 +510,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", dest="cpu_baseline", action="store_false")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-rmse", dest="rmse", action="store_false")
+    ap.add_argument("--no-big", dest="big", action="store_false",
+                    help="skip the configs[3]/[4] (1e9-rating, rank-128) objects")
+    ap.add_argument("--big-steps", type=int, default=3,
+                    help="timed iterations of configs[3] (at most --steps)")
     ap.add_argument("--chunks", type=int, default=None,
-                    help="row chunks per rank for the overlapped all-gathers (default 4 at N>1)")
+                    help="row chunks per rank for the overlapped all-gathers (N>1)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the sharded (RCCL) code path even with one rank")
     args = ap.parse_args()

@@ -98,6 +98,13 @@ class HipKernels:
         return self.E.ld_for(rank)
 
 
+# Largest message of one collective call.  The factor all-gathers and the one-time
+# rating routing at configs[3] scale move several GB per call; every call is kept
+# at or below this (an int32 element/byte count anywhere in a transport would
+# otherwise overflow at 2 GiB).
+MAX_COLLECTIVE_BYTES = 1 << 30
+
+
 def _ranges(deg: torch.Tensor, world: int):
     """Contiguous nnz-balanced row ranges: start[w] .. start[w+1]."""
     n = deg.numel()
@@ -226,10 +233,14 @@ class ShardedALS:
     # ---- setup helpers ----
     def _auto_chunks(self, u_space: int, i_space: int) -> int:
         """4 row chunks when a rank's share of the larger id space reaches 1M rows
-        (the all-gather then moves >= 256 MB per rank at rank 64), else 1."""
+        (the all-gather then moves >= 256 MB per rank at rank 64), else 1; and at
+        least enough chunks that one chunk's all-gather (all ranks, rank <= 128
+        factors, 512 B per row) stays within MAX_COLLECTIVE_BYTES."""
+        big = max(u_space, i_space)
+        need = -(-big * 512 // MAX_COLLECTIVE_BYTES)
         if self.world == 1:
-            return 1
-        return 4 if max(u_space, i_space) // self.world >= (1 << 20) else 1
+            return max(1, need)
+        return max(4 if big // self.world >= (1 << 20) else 1, need)
 
     def _layout(self, ids: torch.Tensor, space: int, offset: int) -> SideLayout:
         dev = self.device
@@ -275,10 +286,36 @@ class ShardedALS:
         out = []
         for t in (a, b, v):
             t = t[order].contiguous()
-            o = torch.empty(sum(rc), dtype=t.dtype, device=t.device)
-            dist.all_to_all_single(o, t, rc, sc, group=self.group)
-            out.append(o)
+            out.append(self._all_to_all_v(t, sc, rc, send_counts.device))
         return out
+
+    def _all_to_all_v(self, t: torch.Tensor, sc, rc, dev) -> torch.Tensor:
+        """all_to_all_single in rounds: round j moves elements [j*C, (j+1)*C) of every
+        peer segment, with C chosen so one call stays within MAX_COLLECTIVE_BYTES.
+        The round count is the max over ranks (every rank issues the same calls)."""
+        W = self.world
+        o = torch.empty(sum(rc), dtype=t.dtype, device=t.device)
+        per = max(1, MAX_COLLECTIVE_BYTES // (t.element_size() * W))
+        rounds_t = torch.tensor([-(-max(max(sc), max(rc), 1) // per)], dtype=torch.int64,
+                                device=dev)
+        dist.all_reduce(rounds_t, op=dist.ReduceOp.MAX, group=self.group)
+        rounds = max(1, int(rounds_t.item()))
+        if rounds == 1:
+            dist.all_to_all_single(o, t, rc, sc, group=self.group)
+            return o
+        soff = [sum(sc[:w]) for w in range(W)]
+        roff = [sum(rc[:w]) for w in range(W)]
+        for j in range(rounds):
+            s_ = [max(0, min(per, sc[w] - j * per)) for w in range(W)]
+            r_ = [max(0, min(per, rc[w] - j * per)) for w in range(W)]
+            send = torch.cat([t[soff[w] + j * per: soff[w] + j * per + s_[w]] for w in range(W)])
+            recv = torch.empty(sum(r_), dtype=t.dtype, device=t.device)
+            dist.all_to_all_single(recv, send, r_, s_, group=self.group)
+            pos = 0
+            for w in range(W):
+                o[roff[w] + j * per: roff[w] + j * per + r_[w]] = recv[pos: pos + r_[w]]
+                pos += r_[w]
+        return o
 
     @property
     def n_users(self) -> int:

@@ -204,3 +204,41 @@ def test_sharded_als_matches_single_process(tmp_path, implicit, chunks):
     assert d["u_starts"][0] == 0 and d["u_starts"][-1] == len(uids)
     assert d["i_starts"][-1] == len(iids)
     assert all(x > 0 for x in np.diff(d["u_starts"]))
+
+
+def _route_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x import distributed as Dm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
+    sel = np.arange(len(u)) % world == rank
+    ref = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=2)
+    Dm.MAX_COLLECTIVE_BYTES = 64  # forces many routing rounds and many chunks
+    small = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
+    ok = small.chunks >= 2
+    for a, b in ((ref.user_blocks, small.user_blocks), (ref.item_blocks, small.item_blocks)):
+        ok = ok and sum(x[0][-1] for x in a if x is not None) == \
+            sum(x[0][-1] for x in b if x is not None)
+    small.fit(4, 2, 0.1, U0_global=None, seed=3)
+    ref.fit(4, 2, 0.1, seed=3)
+    _, Ua = ref.user_factors()
+    _, Ub = small.user_factors()
+    np.save(os.path.join(out_dir, f"route_{rank}.npy"),
+            np.array([float(ok), float(np.abs(Ua.numpy() - Ub.numpy()).max())]))
+    dist.destroy_process_group()
+
+
+def test_chunked_collectives_match(tmp_path):
+    """Routing in several all_to_all rounds and factor all-gathers in more chunks
+    (MAX_COLLECTIVE_BYTES lowered) give the same blocks and the same fit."""
+    mp.spawn(_route_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for w in range(2):
+        ok, diff = np.load(tmp_path / f"route_{w}.npy")
+        assert ok == 1.0 and diff <= 1e-5

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import json
 import os
+import shutil
 import time
 from typing import Dict, Tuple
 
@@ -30,6 +31,13 @@ import numpy as np
 MLLIB_CLASS = "org.apache.spark.mllib.recommendation.MatrixFactorizationModel"
 ML_CLASS = "org.apache.spark.ml.recommendation.ALSModel"
 FORMAT_VERSION = "1.0"
+# DefaultParamsReader parses sparkVersion with VersionUtils.majorMinorVersion and,
+# from 2.4 on, expects a defaultParamMap next to paramMap.
+SPARK_VERSION = "3.5.0"
+# ALSModel's own params (ALSModelParams) and their defaults: the only keys
+# DefaultParamsWriter records for the model.
+ML_MODEL_DEFAULTS = {"blockSize": 4096, "coldStartStrategy": "nan", "itemCol": "item",
+                     "predictionCol": "prediction", "userCol": "user"}
 
 
 def _pa():
@@ -100,9 +108,16 @@ def _read_metadata(path: str) -> Dict:
 
 
 def _check_target(path: str, overwrite: bool) -> None:
-    if os.path.exists(path) and os.listdir(path) and not overwrite:
-        # Spark: "Path ... already exists" unless write.overwrite()
-        raise FileExistsError(f"Path {path} already exists")
+    """Spark: "Path ... already exists" unless write.overwrite(), which deletes the
+    path first (stale part files must not be read back with the new ones)."""
+    if os.path.lexists(path):
+        if not overwrite and (not os.path.isdir(path) or os.listdir(path)):
+            raise FileExistsError(f"Path {path} already exists")
+        if overwrite:
+            if os.path.isdir(path) and not os.path.islink(path):
+                shutil.rmtree(path)
+            else:
+                os.remove(path)
 
 
 def save_mllib(path: str, rank: int, user_ids, U, product_ids, V, overwrite: bool = False) -> None:
@@ -128,12 +143,14 @@ def load_mllib(path: str):
 
 def save_ml(path: str, uid: str, params: Dict, rank: int, user_ids, U, item_ids, V,
             overwrite: bool = False) -> None:
-    """ALSModel.write.save(path): metadata (paramMap) + userFactors + itemFactors (fp32)."""
+    """ALSModel.write.save(path): metadata (paramMap of the set model params,
+    defaultParamMap) + userFactors + itemFactors (fp32)."""
     _check_target(path, overwrite)
     pa, _ = _pa()
+    set_params = {k: v for k, v in params.items() if k in ML_MODEL_DEFAULTS}
     _write_metadata(path, {"class": ML_CLASS, "timestamp": int(time.time() * 1000),
-                           "sparkVersion": "mi355x", "uid": uid, "paramMap": params,
-                           "rank": int(rank)})
+                           "sparkVersion": SPARK_VERSION, "uid": uid, "paramMap": set_params,
+                           "defaultParamMap": dict(ML_MODEL_DEFAULTS), "rank": int(rank)})
     _write_factors(os.path.join(path, "userFactors"), user_ids, U, np.float32, pa.float32())
     _write_factors(os.path.join(path, "itemFactors"), item_ids, V, np.float32, pa.float32())
 

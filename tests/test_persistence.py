@@ -42,8 +42,15 @@ def test_ml_round_trip_and_params(tmp_path):
     path = str(tmp_path / "alsmodel")
     params = {"rank": 5, "regParam": 0.1, "coldStartStrategy": "drop"}
     P.save_ml(path, "ALS_0001", params, 5, uids, U, iids, V)
+    meta = json.loads(open(os.path.join(path, "metadata", "part-00000")).readline())
+    # DefaultParamsWriter: a parseable sparkVersion, the model's set params only, and
+    # the model's defaults in defaultParamMap
+    major, minor = (int(x) for x in meta["sparkVersion"].split(".")[:2])
+    assert (major, minor) >= (2, 4)
+    assert meta["defaultParamMap"] == P.ML_MODEL_DEFAULTS
     uid, p2, rank, u2, U2, i2, V2 = P.load_ml(path)
-    assert uid == "ALS_0001" and p2 == params and rank == 5 and U2.dtype == np.float32
+    assert uid == "ALS_0001" and p2 == {"coldStartStrategy": "drop"} and rank == 5
+    assert U2.dtype == np.float32
     np.testing.assert_array_equal(U2, U[np.argsort(uids)])
     np.testing.assert_array_equal(V2, V[np.argsort(iids)])
 
@@ -55,9 +62,16 @@ def test_existing_path_and_overwrite(tmp_path):
     P.save_mllib(path, 2, uids, U, uids, U)
     with pytest.raises(FileExistsError):
         P.save_mllib(path, 2, uids, U, uids, U)
+    # a stale part file from an earlier (e.g. multi-partition) save must not survive
+    stale = os.path.join(path, "data", "user", "part-00001.parquet")
+    os.replace(os.path.join(path, "data", "user", "part-00000.parquet"), stale)
     P.save_mllib(path, 2, uids, 2 * U, uids, U, overwrite=True)
+    assert not os.path.exists(stale)
     np.testing.assert_array_equal(P.load_mllib(path)[2].astype(np.float32),
                                   (2 * U)[np.argsort(uids)])
+    open(str(tmp_path / "f"), "w").close()  # a plain file in the way
+    with pytest.raises(FileExistsError):
+        P.save_mllib(str(tmp_path / "f"), 2, uids, U, uids, U)
 
 
 def test_wrong_class_and_bad_rank(tmp_path):

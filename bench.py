@@ -97,15 +97,20 @@ def gather_bytes(nnz: int, n_rows: int, k: int) -> float:
     return nnz * (4 * k + 8) + n_rows * (4 * k + 8)
 
 
-def load_pmc(kernel: str):
+def load_pmc(kernel: str, prefix: bool = False):
     """Per-launch rocprofv3 counters of `kernel` from the committed summary
-    (tools/pmc_fold.py over profiles/r02_*), or None."""
+    (tools/gpu_pmc_r02.sh -> tools/pmc_fold.py), or None.  prefix=True: the first
+    kernel whose name starts with `kernel` (template arguments not known here)."""
     try:
         with open(PMC_FILE) as f:
-            d = json.load(f)
-        return d.get("kernels", {}).get(kernel.replace(" ", ""))
+            ks = json.load(f).get("kernels", {})
     except Exception:
         return None
+    name = kernel.replace(" ", "")
+    if not prefix:
+        return ks.get(name)
+    hits = sorted(k_ for k_ in ks if k_.startswith(name))
+    return ks[hits[0]] if hits else None
 
 
 def roofline(kernel: str, launch_ms: dict, nnz_rows: list, k: int, implicit: bool):
@@ -141,6 +146,13 @@ def roofline(kernel: str, launch_ms: dict, nnz_rows: list, k: int, implicit: boo
                                              "write_bytes", "pmc_run_avg_ns", "eff_clock_ghz")
                       if k_ in pmc}
         out["pmc"]["source"] = os.path.relpath(PMC_FILE, ROOT)
+        if traffic:
+            tb = traffic / (1e-6 * out["avg_launch_us"]) / 1e9
+            out["pmc_traffic_view"] = {"bytes_per_launch": traffic, "achieved_gbs": tb,
+                                       "peak_gbs": PEAK_HBM_GBS, "frac": tb / PEAK_HBM_GBS,
+                                       "note": "L2 memory-side bytes (FETCH_SIZE x2 + WRITE_SIZE); "
+                                               "below the algorithmic bytes = factor rows "
+                                               "re-read from L2 / Infinity Cache"}
         busy = {"valu": pmc.get("valu_busy_frac"), "mfma": pmc.get("mfma_busy_frac"),
                 "hbm": (traffic / (1e-6 * out["avg_launch_us"]) / 1e9 / PEAK_HBM_GBS)
                 if traffic else None}
@@ -161,7 +173,8 @@ def roofline(kernel: str, launch_ms: dict, nnz_rows: list, k: int, implicit: boo
 
 def topk_roofline(n_q: int, n_v: int, k: int, ms: float, top: int):
     useful = 2.0 * n_q * n_v * k
-    issued = 3.0 * 2.0 * n_q * n_v * kp_of(k)
+    kq = max(32, kp_of(k))  # topk_kq (csrc/topk.hip): dims padded to 32/64/128
+    issued = 3.0 * 2.0 * n_q * n_v * kq
     s = ms * 1e-3
     out = {"kernel": "topk_split_kernel", "top": top, "n_q": n_q, "n_v": n_v, "rank": k,
            "ms": ms, "recs_per_s": n_q / s,
@@ -169,9 +182,14 @@ def topk_roofline(n_q: int, n_v: int, k: int, ms: float, top: int):
            "issued_f16_mfma_tflops": issued / s / 1e12,
            "mfma_frac": issued / s / 1e12 / PEAK_F16_MFMA_TFLOPS,
            "bound": "mfma", "unit": "TFLOP/s"}
-    pmc = load_pmc("topk_split_kernel")
+    pmc = load_pmc(f"topk_split_kernel<{kq // 32},", prefix=True)
     if pmc:
-        out["pmc_mfma_busy_frac"] = pmc.get("mfma_busy_frac")
+        out["pmc"] = {k_: pmc.get(k_) for k_ in ("mfma_busy_frac", "valu_busy_frac",
+                                                 "pmc_run_avg_ns")}
+        busy = {"valu": pmc.get("valu_busy_frac"), "mfma": pmc.get("mfma_busy_frac")}
+        busy = {k_: v for k_, v in busy.items() if v is not None}
+        if busy:
+            out["limiter"] = max(busy, key=busy.get)
     return out
 
 

@@ -2,6 +2,12 @@
 averages (one entry per short kernel name), plus derived utilisation figures.
 
     python tools/pmc_fold.py OUT.json DIR_OR_CSV [DIR_OR_CSV ...]
+    python tools/pmc_fold.py OUT.json TAG=DIR[,DIR...] [TAG=DIR[,DIR...] ...]
+
+The second form folds each group (one workload's passes) separately and merges
+them; a kernel name present in several groups keeps the FIRST group's entry
+(e.g. topk_split_kernel of the rank-64 run).  OUT.json = {"kernels": {...},
+"groups": {kernel: tag}, "sources": {tag: [dirs]}}.
 
 Derived (MI355X_MICROARCH.md "PMC" and "DVFS" notes):
   * GRBM_GUI_ACTIVE is summed over the 8 XCDs -> per-XCD busy cycles = /8.
@@ -61,6 +67,14 @@ def fold(paths):
         g = ent.get("GRBM_GUI_ACTIVE")
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in ent:
             ent["mfma_busy_frac"] = ent["SQ_VALU_MFMA_BUSY_CYCLES"] / (N_SIMD * g / 8)
+        if g and "SQ_ACTIVE_INST_VALU" in ent:  # quad-cycles per wave
+            ent["valu_busy_frac"] = 4 * ent["SQ_ACTIVE_INST_VALU"] / (N_SIMD * g / 8)
+        if g and "SQ_INSTS_VALU" in ent:  # 4 issue cycles per wave64 instruction
+            ent["valu_issue_frac"] = 4 * ent["SQ_INSTS_VALU"] / (N_SIMD * g / 8)
+        if "SQ_WAVE_CYCLES" in ent and ent["SQ_WAVE_CYCLES"] > 0:
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                if c in ent:
+                    ent[c.lower().replace("sq_", "") + "_frac_of_wave"] = ent[c] / ent["SQ_WAVE_CYCLES"]
         if g and "pmc_run_avg_ns" in ent:
             ent["eff_clock_ghz"] = (g / 8) / ent["pmc_run_avg_ns"]
         if "FETCH_SIZE" in ent:
@@ -77,9 +91,22 @@ def fold(paths):
 
 def main():
     dst = sys.argv[1]
-    res = fold(files(sys.argv[2:]))
+    args = sys.argv[2:]
+    if args and all("=" in a for a in args):
+        res, groups, sources = {}, {}, {}
+        for a in args:
+            tag, dirs = a.split("=", 1)
+            dirs = dirs.split(",")
+            sources[tag] = [os.path.basename(d.rstrip("/")) for d in dirs]
+            for k, v in fold(files(dirs)).items():
+                if k not in res:
+                    res[k], groups[k] = v, tag
+        doc = {"kernels": res, "groups": groups, "sources": sources}
+    else:
+        res = fold(files(args))
+        doc = {"kernels": res}
     with open(dst, "w") as f:
-        json.dump(res, f, indent=1, sort_keys=True)
+        json.dump(doc, f, indent=1, sort_keys=True)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1].get("pmc_run_avg_ns", 0))[:12]:
         print(k, {c: (round(x, 4) if isinstance(x, float) else x) for c, x in v.items()})
 

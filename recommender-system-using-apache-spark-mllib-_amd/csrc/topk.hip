@@ -18,12 +18,11 @@
 // ds_read_b128.  The query rows are split in registers once per workgroup.
 //
 // Workgroup = 4 wavefronts x RG row groups = 64 RG query rows.  The workgroup
-// sweeps V in 64-row tiles staged in LDS (rows padded by 16 B: the 16 lanes
-// of a row-group read distinct bank slots); the next tile's global loads are
-// in flight while the current one is scored.  Per tile each wave computes
-// RG 16 x 64 score blocks, then filters each against its rows' current k-th
-// best (score, index) and inserts the rare survivors into a sorted list in
-// LDS with a wave-cooperative insertion.  Order: score descending, ties by
+// sweeps V in tiles double-buffered in LDS (one barrier per tile, the loads of
+// the tile after next in flight).  Per 16 V rows each wave computes RG 16 x 16
+// score blocks, filters them against its rows' current k-th best score and
+// inserts the rare survivors into a sorted list in LDS with a wave-cooperative
+// insertion.  Order: score descending, ties by
 // ascending index (the build's deterministic tie rule).
 // Scores are compared in the scaled domain (exact: powers of two) and
 // unscaled on output.
@@ -214,7 +213,57 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 
 // Split-f16 scores.  NK = KQ / 32 MFMA k-steps (KQ = k padded to 32, 64 or 128);
 // RG query-row groups of 64 per workgroup.  scal[0] = max |Q|, scal[1] = max |V|.
-template <int NK, int RG>
+//
+// V is swept in tiles of kTkVT(NK) rows, double-buffered in LDS: tile t+1 is
+// written (from registers loaded one tile earlier) while nothing reads its
+// buffer, so ONE barrier per tile; the global loads of tile t+2 are then in
+// flight during tile t+1's MFMAs.  LDS rows are RW + 2 uint4 apart: the
+// ds_read_b128 lane groups of gfx950 ({0-3,12-15,20-27}, ...) then touch 16
+// distinct 4-bank slots (row stride = 2 mod 16 slots), conflict-free.
+// Filter: the (score, index) k-th of a full list always has a smaller index than
+// the V rows being scored (V is swept in index order), so a candidate can beat
+// it only if score >= k-th score: one compare per score, one ballot per 16 x 16
+// block; the exact (score, index) insertion runs only for blocks with a
+// survivor.  The MFMAs of block c+1 are issued before block c's filter (two
+// accumulator sets).
+// Lists (TOPR > 0, top <= TOPR): each row's list lives in the registers of one
+// "owner" lane (lane 16g + rho owns row rho of group g), sorted by ascending
+// goodness with the k-th best at [0] (entries top..TOPR-1 are sentinels that
+// nothing beats), so the threshold is a fixed register and an insertion is one
+// branch-free bubble pass.  A block with survivors stages its 16 x 16 scores in
+// LDS (one ds_write_b128 per lane); each owner lane takes its row's survivors
+// from the ballots, inserts them, and the new k-th scores go back to the
+// filtering lanes by ds_bpermute.  TOPR = 0 (larger top): sorted lists in LDS,
+// wave-cooperative insertion (topk_offer).
+__host__ __device__ constexpr int tk_vt(int nk) { return 128 / nk; }
+
+// Insert candidate (sc, id) into a list sorted by ascending goodness (k-th best at
+// [0]; entries past `top` are sentinels (+inf, -1) that nothing beats; unfilled
+// entries are (-inf, INT_MAX)).  Every list index is below `id` (V is swept in
+// index order), so the candidate beats entry j iff sc > its score or the entry
+// is unfilled.  c_j is monotone (true for j < p); the list becomes
+// [.. entries 1..p-1, candidate, entries p..]: independent selects, no chain.
+// The caller has checked that the candidate beats [0] and is not NaN.
+template <int TOPR>
+__device__ __forceinline__ void tk_insert(float (&sv)[TOPR], int (&iv)[TOPR], float sc, int id) {
+  bool c[TOPR + 1];
+#pragma unroll
+  for (int j = 0; j < TOPR; ++j) c[j] = sc > sv[j] || iv[j] == 0x7fffffff;
+  c[TOPR] = false;
+#pragma unroll
+  for (int j = 0; j < TOPR; ++j) {
+    const float sn = j + 1 < TOPR ? sv[j + 1] : 0.f;
+    const int in = j + 1 < TOPR ? iv[j + 1] : 0;
+    sv[j] = c[j + 1] ? sn : (c[j] ? sc : sv[j]);
+    iv[j] = c[j + 1] ? in : (c[j] ? id : iv[j]);
+  }
+}
+
+// MODE (dev ablation only, tools/dev_topk.hip; the product launches MODE 0):
+// 1 = scores only (no filter), 2 = filter against an unbeatable threshold (no
+// insertions), 3 = as 0 but each wave writes its count of exact-insertion calls
+// to score_out[wave] instead of the lists.
+template <int NK, int RG, int TOPR, int MODE = 0>
 __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
                                                          int64_t n_v, int ld, int k, int top,
@@ -222,14 +271,20 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
                                                          int32_t* __restrict__ idx_out,
                                                          float* __restrict__ score_out) {
   constexpr int KQ = 32 * NK;
-  constexpr int RW = KQ / 4;          // uint4 per split row (KQ hi + KQ lo halves)
-  constexpr int RS = RW + 1;          // LDS row stride in uint4 (16-B pad)
-  constexpr int PER = 64 * RW / 256;  // staged uint4 per thread per tile
+  constexpr int RW = KQ / 4;           // uint4 per split row (KQ hi + KQ lo halves)
+  constexpr int RS = RW + 2;           // LDS row stride in uint4 (bank-conflict-free)
+  constexpr int VT = tk_vt(NK);        // V rows per tile
+  constexpr int NC = VT / 16;          // 16-row score blocks per tile
+  constexpr int PER = VT * RW / 256;   // staged uint4 per thread per tile
+  static_assert(PER * 256 == VT * RW, "tile staging");
   extern __shared__ uint4 smem_u4[];
-  uint4* tile = smem_u4;                                 // [64][RS]
-  float* ls = reinterpret_cast<float*>(tile + 64 * RS);  // [64 RG rows][top] scores
-  int* li = reinterpret_cast<int*>(ls + 64 * RG * top);  // [64 RG rows][top] indices
-  int* len = li + 64 * RG * top;                         // [64 RG]
+  uint4* tiles = smem_u4;                                     // [2][VT][RS]
+  // TOPR == 0: [64 RG rows][top] scores, indices, [64 RG] lengths
+  // TOPR > 0: per wave and group a 16 x 16 score block [item m][row]
+  float* ls = reinterpret_cast<float*>(tiles + 2 * VT * RS);
+  int* li = reinterpret_cast<int*>(ls + 64 * RG * top);
+  int* len = li + 64 * RG * top;
+  float* sblk = ls;
 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   const int64_t qbase = (int64_t)blockIdx.x * 64 * RG;
@@ -256,7 +311,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
     }
   }
-  if (threadIdx.x < 64 * RG) len[threadIdx.x] = 0;
+  if (TOPR == 0 && threadIdx.x < 64 * RG) len[threadIdx.x] = 0;
   float ts[RG][4];
   int ti[RG][4];
 #pragma unroll
@@ -266,6 +321,16 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       ts[g][r] = -__builtin_inff();
       ti[g][r] = 0x7fffffff;
     }
+  bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
+  // TOPR > 0: this lane's row list (owner lanes lane < 16 RG)
+  constexpr int NR = TOPR > 0 ? TOPR : 1;
+  float lsv[NR];
+  int liv[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    lsv[j] = j < top ? -__builtin_inff() : __builtin_inff();
+    liv[j] = j < top ? 0x7fffffff : -1;
+  }
 
   uint4 pre[PER];
   auto fetch = [&](int64_t vb) {
@@ -276,42 +341,153 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW] : make_uint4(0u, 0u, 0u, 0u);
     }
   };
-  fetch(0);
-  for (int64_t vb = 0; vb < n_v; vb += 64) {
-    __syncthreads();
+  auto stage = [&](int buf) {
+    uint4* t = tiles + buf * VT * RS;
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int x = threadIdx.x + 256 * e;
-      tile[(x / RW) * RS + x % RW] = pre[e];
+      t[(x / RW) * RS + x % RW] = pre[e];
     }
-    __syncthreads();
-    if (vb + 64 < n_v) fetch(vb + 64);
+  };
+  auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {
+    // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      // B operand: lane (q, m) holds dims 32s + 8q .. +7 of V row vb + 16c + m
-      const uint4* tb = tile + (16 * c + m) * RS;
-      floatx4 acc[RG];
+    for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < NK; ++s) {
+      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+      const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[KQ / 8 + 4 * s + q]);
 #pragma unroll
-      for (int s = 0; s < NK; ++s) {
-        const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
-        const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[KQ / 8 + 4 * s + q]);
-#pragma unroll
-        for (int g = 0; g < RG; ++g) {
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bl, acc[g], 0, 0, 0);
-          acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[g][s], bh, acc[g], 0, 0, 0);
-        }
+      for (int g = 0; g < RG; ++g) {
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bl, acc[g], 0, 0, 0);
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[g][s], bh, acc[g], 0, 0, 0);
       }
-      // acc[g][r] = scaled score(row 64g + 16w + 4q + r, V row vb + 16c + m)
+    }
+  };
+  float sink = 0.f;
+  int n_offer = 0;
+  auto filter = [&](const floatx4 (&acc)[RG], int64_t ibase) {
+    // acc[g][r] = scaled score(row 64g + 16w + 4q + r, V row ibase + m)
+    if constexpr (MODE == 1) {
+#pragma unroll
+      for (int g = 0; g < RG; ++g) sink += fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
+      return;
+    }
+    const bool vin = ibase + m < n_v;
+    if constexpr (TOPR > 0) {
+      // full lists: strict > (a tie at the k-th score has a larger index); until
+      // then every block goes to the owner lanes (exact beats() there)
+      bool pr[RG][4];
+      bool anyl = false;
 #pragma unroll
       for (int g = 0; g < RG; ++g)
-        topk_offer(acc[g], (int)(vb + 16 * c), n_v, ts[g], ti[g], ls, li, len, 64 * g + 16 * w,
-                   top);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pr[g][r] = vin && (!full || acc[g][r] > (MODE == 2 ? 3.0e38f : ts[g][r]));
+          anyl = anyl || pr[g][r];
+        }
+      if (__ballot(anyl) == 0) return;
+      if constexpr (MODE == 3) ++n_offer;
+      float* st = sblk + w * RG * 256;              // [g][item m][row]
+      float* thr = sblk + 4 * RG * 256 + w * RG * 16;  // [g][row] new k-th scores
+      uint64_t b[RG][4];
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        *reinterpret_cast<floatx4*>(st + g * 256 + 16 * m + 4 * q) = acc[g];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[g][r] = __ballot(pr[g][r]);
+      }
+      asm volatile("" ::: "memory");  // LDS is in order within the wave
+      if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
+        const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
+        uint64_t bb = b[0][0];
+#pragma unroll
+        for (int t = 1; t < 4 * RG; ++t) bb = sel == t ? b[t / 4][t % 4] : bb;
+        unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
+        const float* sg = st + g * 256 + rho;
+        while (msk) {
+          const int mm = __builtin_ctz(msk);
+          msk &= msk - 1;
+          const float sc = sg[16 * mm];
+          const int id = (int)ibase + mm;
+          if (beats(sc, id, lsv[0], liv[0])) tk_insert<NR>(lsv, liv, sc, id);
+        }
+        thr[lane] = lsv[0];
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
+        ts[g][0] = t4[0]; ts[g][1] = t4[1]; ts[g][2] = t4[2]; ts[g][3] = t4[3];
+      }
+      if (!full) full = __ballot(lane < 16 * RG && liv[0] == 0x7fffffff) == 0;
+      return;
     }
-  }
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      bool hit = !full;
+      if (full) {
+        const bool p = vin && (acc[g][0] > ts[g][0] || acc[g][1] > ts[g][1] ||
+                               acc[g][2] > ts[g][2] || acc[g][3] > ts[g][3]);
+        hit = __ballot(p) != 0;
+      }
+      if constexpr (MODE == 3) n_offer += hit ? 1 : 0;
+      if (hit)
+        topk_offer(acc[g], (int)ibase, n_v, ts[g], ti[g], ls, li, len, 64 * g + 16 * w, top);
+    }
+    if (!full) {
+      bool f = true;
+      if (lane < 16 * RG) f = len[64 * (lane >> 4) + 16 * w + (lane & 15)] >= top;
+      full = __ballot(!f) == 0;
+    }
+  };
+
+  fetch(0);
+  stage(0);
   __syncthreads();
+  if (VT < n_v) fetch(VT);
+  int buf = 0;
+  for (int64_t vb = 0; vb < n_v; vb += VT) {
+    const uint4* tb = tiles + buf * VT * RS;
+    floatx4 acc0[RG], acc1[RG];
+    score(tb + m * RS, acc0);
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      // issue block c+1's MFMAs, then filter block c
+      if (c % 2 == 0) {
+        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc1);
+        filter(acc0, vb + 16 * c);
+      } else {
+        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc0);
+        filter(acc1, vb + 16 * c);
+      }
+    }
+    if (vb + VT < n_v) stage(buf ^ 1);
+    __syncthreads();
+    if (vb + 2 * VT < n_v) fetch(vb + 2 * VT);
+    buf ^= 1;
+  }
+  if constexpr (MODE != 0) {
+    if (lane == 0) score_out[blockIdx.x * 4 + w] = MODE == 1 ? sink : (float)n_offer;
+    return;
+  }
+  if constexpr (TOPR > 0) {
+    if (lane < 16 * RG) {
+      const int64_t row = qbase + 64 * (lane >> 4) + 16 * w + (lane & 15);
+      if (row < n_q) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+          if (j < top) {
+            const bool real = liv[j] != 0x7fffffff;
+            idx_out[row * top + (top - 1 - j)] = real ? liv[j] : -1;
+            score_out[row * top + (top - 1 - j)] = real ? lsv[j] * unscale : -__builtin_inff();
+          }
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int g = 0; g < RG; ++g)
     topk_write(ls, li, len, 64 * g + 16 * w, qbase, n_q, top, unscale, idx_out, score_out);
@@ -403,8 +579,13 @@ static size_t topk_lds_bytes(int cn, int top) {
 
 static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
 
+constexpr int kTopR = 16;  // register-resident lists for top <= kTopR
+
 static size_t topk_split_lds_bytes(int kq, int rg, int top) {
-  return 16 * 64 * (size_t)(kq / 4 + 1) + (sizeof(float) + sizeof(int)) * 64 * (size_t)rg * top +
+  const int nk = kq / 32;
+  const size_t tiles = 16 * 2 * (size_t)tk_vt(nk) * (size_t)(kq / 4 + 2);
+  if (top <= kTopR) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
+  return tiles + (sizeof(float) + sizeof(int)) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
 }
 
@@ -489,13 +670,20 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   const size_t lds = topk_split_lds_bytes(kq, rg, top);
   const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
   const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
-#define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                                                           \
+#define ALS_TOPK_SPLIT_LAUNCH2(NK, RG, TR)                                                      \
   do {                                                                                          \
-    ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG>),      \
+    ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, TR>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
-    topk_split_kernel<NK, RG><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, scal,      \
-                                                      idx_out, score_out);                      \
+    topk_split_kernel<NK, RG, TR><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, scal,  \
+                                                          idx_out, score_out);                  \
     ALS_LAUNCH_CHECK();                                                                         \
+  } while (0)
+#define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                 \
+  do {                                                \
+    if (top <= kTopR)                                 \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
+    else                                              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);
@@ -508,6 +696,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     else ALS_TOPK_SPLIT_LAUNCH(4, 1);
   }
 #undef ALS_TOPK_SPLIT_LAUNCH
+#undef ALS_TOPK_SPLIT_LAUNCH2
   return ALS_OK;
 }
 

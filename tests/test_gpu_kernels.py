@@ -313,7 +313,7 @@ def test_compute_error_kat_on_gpu():
 
 
 # ---------------------------------------------------------------- K5
-@pytest.mark.parametrize("rank,top", [(4, 1), (10, 10), (32, 20), (64, 10), (64, 100),
+@pytest.mark.parametrize("rank,top", [(4, 1), (10, 10), (32, 20), (64, 10), (64, 16), (16, 17), (64, 100),
                                       (64, 256), (96, 10), (128, 100), (128, 253)])
 def test_topk_parity(rank, top):
     rng = np.random.default_rng(rank * 1000 + top)
@@ -341,6 +341,40 @@ def test_topk_parity(rank, top):
     for r_ in both:
         lst = list(idx[r_])
         assert lst.index(10) < lst.index(20)
+
+
+@pytest.mark.parametrize("rank,n_v", [(64, 20011), (128, 9001), (32, 17), (16, 300)])
+def test_topk_many_tiles_ties_across_tiles(rank, n_v):
+    """Many V tiles, a ragged last tile, and exact ties whose copies sit in different
+    tiles and blocks (the lower index must win wherever the copies fall)."""
+    rng = np.random.default_rng(rank + n_v)
+    n_q, top = 261, 10
+    Q = rng.standard_normal((n_q, rank)).astype(np.float32)
+    Vm = rng.standard_normal((n_v, rank)).astype(np.float32)
+    Vm *= (1.0 + 3.0 * (np.arange(n_v) % 97 == 0))[:, None].astype(np.float32)  # strong items
+    pairs = [(a, b) for a, b in ((0, n_v - 1), (5, 4100), (130, 131), (97, 9000)) if b < n_v]
+    for a, b in pairs:
+        Vm[b] = Vm[a]
+    ld = E.ld_for(rank)
+    Qd = torch.zeros((n_q, ld), device=DEV)
+    Qd[:, :rank] = torch.as_tensor(Q).to(DEV)
+    Vd = torch.zeros((n_v, ld), device=DEV)
+    Vd[:, :rank] = torch.as_tensor(Vm).to(DEV)
+    idx, sc = E.topk_rows(Qd, n_q, Vd, n_v, rank, top)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    ref_i, ref_s = O.topk(Q, Vm, top)
+    S = Q.astype(np.float64) @ Vm.astype(np.float64).T
+    for row in range(n_q):
+        if not np.array_equal(idx[row], ref_i[row]):
+            bad = np.nonzero(idx[row] != ref_i[row])[0]
+            for p_ in bad:
+                assert abs(S[row, idx[row, p_]] - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
+        np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
+        lst = list(idx[row])
+        for a, b in pairs:
+            if a in lst and b in lst:
+                assert lst.index(a) < lst.index(b)
+    assert any(a in idx[r_] and b in idx[r_] for r_ in range(n_q) for a, b in pairs)
 
 
 def test_topk_fewer_items_than_top():

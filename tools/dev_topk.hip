@@ -1,0 +1,57 @@
+// Dev-only (NOT part of libals_hip.so): topk_split_kernel ablation modes, timed by
+// tools/topk_ablate.py.  mode 0 = the product als_topk; modes 1 / 3 reuse the
+// split table that a preceding mode-0 call left in the workspace:
+//   1: scores only (no filter)   3: product filter, counts exact-insertion calls
+#include "../recommender-system-using-apache-spark-mllib-_amd/csrc/topk.hip"
+
+namespace als {
+void set_error(const char*, ...) {}
+}
+
+extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, int64_t n_v, int ld,
+                        int k, int top, int32_t* idx, float* sc, void* ws, size_t ws_bytes,
+                        float* dbg, void* stream) {
+  using namespace als;
+  if (mode == 0) return als_topk(Q, n_q, V, n_v, ld, k, top, idx, sc, ws, ws_bytes, stream);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int kq = topk_kq(k);
+  const int rg = topk_split_rg(k, top);
+  if (rg == 0) return -1;
+  const size_t lds = topk_split_lds_bytes(kq, rg, top);
+  const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
+  const float* scal = reinterpret_cast<const float*>(ws);
+  const uint4* vsp4 = reinterpret_cast<const uint4*>(static_cast<char*>(ws) + 256);
+#define L(NK, RG, M)                                                                          \
+  do {                                                                                        \
+    if (top <= kTopR) {                                                                       \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, kTopR, M>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+      topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, \
+                                                                  scal, idx, dbg);            \
+    } else {                                                                                  \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, 0, M>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+      topk_split_kernel<NK, RG, 0, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, \
+                                                              scal, idx, dbg);                \
+    }                                                                                         \
+  } while (0)
+#define LM(NK, RG) \
+  do {             \
+    if (mode == 1) \
+      L(NK, RG, 1); \
+    else if (mode == 2) \
+      L(NK, RG, 2); \
+    else           \
+      L(NK, RG, 3); \
+  } while (0)
+  if (kq == 64) {
+    if (rg == 2) LM(2, 2); else LM(2, 1);
+  } else if (kq == 128) {
+    if (rg == 2) LM(4, 2); else LM(4, 1);
+  } else {
+    if (rg == 2) LM(1, 2); else LM(1, 1);
+  }
+#undef LM
+#undef L
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

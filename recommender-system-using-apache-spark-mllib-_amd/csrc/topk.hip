@@ -235,7 +235,9 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // from the ballots, inserts them, and the new k-th scores go back to the
 // filtering lanes by ds_bpermute.  TOPR = 0 (larger top): sorted lists in LDS,
 // wave-cooperative insertion (topk_offer).
-__host__ __device__ constexpr int tk_vt(int nk) { return 128 / nk; }
+// Tile rows: 64 / NK keeps the staging registers at 2 x uint4 per thread; larger
+// tiles cost occupancy (measured: 128 / NK and 192 / NK slower on ML-25M shapes).
+__host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
 
 // Insert candidate (sc, id) into a list sorted by ascending goodness (k-th best at
 // [0]; entries past `top` are sentinels (+inf, -1) that nothing beats; unfilled

@@ -97,6 +97,9 @@ class HipKernels:
     def ld(self, rank: int) -> int:
         return self.E.ld_for(rank)
 
+    def block_values(self, block) -> torch.Tensor:
+        return block.val
+
 
 # Largest message of one collective call.  The factor all-gathers and the one-time
 # rating routing at configs[3] scale move several GB per call; every call is kept
@@ -405,13 +408,50 @@ class ShardedALS:
                                "equations are not positive definite (Spark raises from dppsv)")
 
     def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0=None,
-            U0_global=None):
+            U0_global=None, checkpoint_dir=None, checkpoint_interval=10, resume=False):
+        """ALSCore.fit's contract.  Checkpoints hold the dense global factors (written
+        by process 0, read by every rank), so a job may resume on another world size."""
+        from . import checkpoint as C
+        start, Uc, Vc = C.resume_point(checkpoint_dir, resume, self, rank, reg, implicit, alpha,
+                                       max_iter)
+        if Uc is not None:
+            U0, U0_global = None, Uc
         self.init_factors(rank, seed, U0, U0_global)
+        if Vc is not None:
+            self._set_dense(False, Vc)
         self.status.zero_()
-        for _ in range(max_iter):
+        for it in range(start, max_iter):
             self.iterate(reg, implicit, alpha)
+            C.maybe_save(checkpoint_dir, checkpoint_interval, it + 1, self, rank, reg, implicit,
+                         alpha, writer=self.proc == 0)
+        if checkpoint_dir:
+            dist.barrier(group=self.group)
         self.check_status()
         return self
+
+    def _set_dense(self, user_side: bool, F) -> None:
+        """Overwrite one replicated factor table (and this rank's rows) from a dense
+        [n, rank] host/device array (every rank passes the same array)."""
+        side, full, loc = (self.users, self.U_full, self.U_loc) if user_side else \
+            (self.items, self.V_full, self.V_loc)
+        F = torch.as_tensor(F).to(self.device, torch.float32)
+        pad = side.padded(torch.arange(side.n, device=self.device)).long()
+        full[pad, :self.rank] = F
+        loc.copy_(full.view(loc.shape[0], self.world, -1, full.shape[1])[:, self.proc])
+        self._dense_cache = {}
+
+    def fingerprint(self) -> dict:
+        """ALSCore.fingerprint over the ratings of all ranks."""
+        bits = torch.zeros(1, dtype=torch.int64, device=self.device)
+        for blk in self.user_blocks:
+            if blk is not None:
+                bits += self.K.block_values(blk).view(torch.int32).long().sum().to(self.device)
+        dist.all_reduce(bits, group=self.group)
+        return {"nnz": int(self.nnz), "n_users": int(self.n_users), "n_items": int(self.n_items),
+                "rating_bits": int(bits), "item_id_sum": int(self.items.ids().long().sum())}
+
+    def user_factor_ids(self) -> torch.Tensor:
+        return self.users.ids()
 
     # ---- serving protocol (engine.ALSCore's), on the replicated factors ----
     def _dense(self, user_side: bool) -> torch.Tensor:

@@ -393,13 +393,34 @@ class ALSCore:
                 f"Cholesky failed (non-positive pivot) for dense row {s - 1}: the normal "
                 "equations are not positive definite (Spark raises from LAPACK dppsv here)")
 
-    def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0=None):
-        self.init_factors(rank, seed, U0)
+    def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0=None,
+            checkpoint_dir=None, checkpoint_interval=10, resume=False):
+        """max_iter ALS iterations from the seeded (or given U0) start.  checkpoint_dir:
+        write U, V every checkpoint_interval iterations (checkpoint.py); resume
+        (True / "auto"): continue from the checkpoint there at its iteration."""
+        from . import checkpoint as C
+        start, Uc, Vc = C.resume_point(checkpoint_dir, resume, self, rank, reg, implicit, alpha,
+                                       max_iter)
+        self.init_factors(rank, seed, Uc if Uc is not None else U0)
+        if Vc is not None:
+            self.V[:, :rank] = _to_device(Vc, torch.float32, self.device)
         self.status.zero_()
-        for _ in range(max_iter):
+        for it in range(start, max_iter):
             self.iterate(reg, implicit, alpha)
+            C.maybe_save(checkpoint_dir, checkpoint_interval, it + 1, self, rank, reg, implicit,
+                         alpha)
         self.check_status()
         return self
+
+    def fingerprint(self) -> dict:
+        """Order-independent identity of the training ratings (checkpoint matching)."""
+        v = self.user_block.val
+        return {"nnz": int(self.nnz), "n_users": int(self.n_users), "n_items": int(self.n_items),
+                "rating_bits": int(v.view(torch.int32).long().sum()),
+                "item_id_sum": int(self.iidx.ids().long().sum())}
+
+    def user_factor_ids(self) -> torch.Tensor:
+        return self.uidx.ids()
 
     # ---- K4 / K5 (the serving protocol shared with distributed.ShardedALS) ----
     def predict(self, users, items) -> torch.Tensor:

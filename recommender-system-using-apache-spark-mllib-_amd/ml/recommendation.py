@@ -85,13 +85,23 @@ def _make_accessors(cls, names):
 class ALS(_Params):
     """Alternating Least Squares (explicit or implicit feedback) on one MI355X.
 
-    ``numUserBlocks`` / ``numItemBlocks`` / storage levels / ``checkpointInterval``
-    are accepted for signature compatibility and have no effect (the ratings are a
-    single device-resident CSR per side; there is no RDD lineage to checkpoint).
+    ``numUserBlocks`` / ``numItemBlocks`` / storage levels are accepted for signature
+    compatibility and have no effect (the ratings are a single device-resident CSR
+    per side).  ``checkpointInterval`` acts as in Spark once a checkpoint directory
+    is set (``setCheckpointDir``, the role of ``SparkContext.setCheckpointDir``):
+    the factors are written every ``checkpointInterval`` iterations, and a fit of
+    the same ratings and params in that directory resumes from the checkpoint
+    (checkpoint.py) instead of starting over.
     """
 
     def __init__(self, **kw):
         self._init_params(kw)
+        self._checkpoint_dir = None
+
+    def setCheckpointDir(self, path):
+        """Directory for factor checkpoints (None disables)."""
+        self._checkpoint_dir = None if path is None else str(path)
+        return self
 
     def setParams(self, **kw):
         for k, v in kw.items():
@@ -115,7 +125,9 @@ class ALS(_Params):
         seed = _DEFAULT_SEED if p["seed"] is None else int(p["seed"])
         core = _engine.make_engine(u, i, r)
         core.fit(int(p["rank"]), int(p["maxIter"]), float(p["regParam"]),
-                 bool(p["implicitPrefs"]), float(p["alpha"]), seed=seed)
+                 bool(p["implicitPrefs"]), float(p["alpha"]), seed=seed,
+                 checkpoint_dir=self._checkpoint_dir,
+                 checkpoint_interval=int(p["checkpointInterval"]), resume="auto")
         return ALSModel(core, dict(p))
 
 

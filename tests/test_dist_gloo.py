@@ -69,6 +69,9 @@ class OracleKernels:
     def ld(self, rank):
         return rank
 
+    def block_values(self, block):
+        return torch.as_tensor(block[2])
+
 
 def _free_port():
     s = socket.socket()
@@ -242,3 +245,51 @@ def test_chunked_collectives_match(tmp_path):
     for w in range(2):
         ok, diff = np.load(tmp_path / f"route_{w}.npy")
         assert ok == 1.0 and diff <= 1e-5
+
+
+def _resume_worker(rank, world, port, out_dir, mode):
+    """mode "full": 4 iterations; "ckpt": 2 iterations writing a checkpoint every 2;
+    "resume": resume=True to 4 iterations; "at": resume at the checkpoint's own count."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x.distributed import ShardedALS
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r = planted(100, 80, density=0.09, seed=41, heavy_items=(5,))
+    sel = np.arange(len(u)) % world == rank
+    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
+    ck = os.path.join(out_dir, "ckpt")
+    if mode == "full":
+        K.fit(5, 4, 0.1, seed=7)
+    elif mode == "ckpt":
+        K.fit(5, 2, 0.1, seed=7, checkpoint_dir=ck, checkpoint_interval=2)
+    elif mode == "resume":
+        K.fit(5, 4, 0.1, seed=99, checkpoint_dir=ck, checkpoint_interval=0, resume=True)
+    else:  # "at": nothing left to run, U and V come from the checkpoint
+        K.fit(5, 2, 0.1, seed=99, checkpoint_dir=ck, checkpoint_interval=0, resume=True)
+    _, Uf = K.user_factors()
+    _, Vf = K.item_factors()
+    if rank == 0:
+        np.savez(os.path.join(out_dir, f"{mode}_w{world}.npz"), U=Uf.numpy(), V=Vf.numpy())
+    dist.destroy_process_group()
+
+
+def test_checkpoint_resume_across_world_sizes(tmp_path):
+    """A fit checkpointed at iteration 2 on 1 rank and resumed to 4 on 2 ranks gives
+    the uninterrupted 4-iteration factors (the resume's own seed is ignored)."""
+    for mode, world in (("full", 2), ("ckpt", 1), ("resume", 2), ("at", 2)):
+        mp.spawn(_resume_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world,
+                 join=True)
+    full = np.load(tmp_path / "full_w2.npz")
+    res = np.load(tmp_path / "resume_w2.npz")
+    np.testing.assert_array_equal(res["U"], full["U"])
+    np.testing.assert_array_equal(res["V"], full["V"])
+    ck = np.load(tmp_path / "ckpt" / "user_factors.npy")
+    at = np.load(tmp_path / "at_w2.npz")
+    np.testing.assert_array_equal(at["U"], ck)
+    np.testing.assert_array_equal(at["V"], np.load(tmp_path / "ckpt" / "item_factors.npy"))

@@ -34,7 +34,7 @@ namespace als {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kYtyChunk = 8192;      // src rows per YtY task
+constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
 constexpr int kMaxRank = 128;
 
 template <int CN>
@@ -1693,52 +1693,59 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
 // order (+ YtY in fp64 for implicit), one rounding, then the solve.  Entries are
 // reduced 16 at a time (a memory clobber keeps the groups' slot loops apart, so
 // only 16 fp64 sums are live).
+// Launch 2a: the fp32 chunk slots of every heavy row summed in fp64 (element-wise,
+// one thread per slot element; fixed order: four interleaved partial sums),
+// the implicit YtY added in fp64, then rounded once to fp32 into the row's first
+// slot (each thread reads and writes only its own element: in place is safe).
+template <bool IMPLICIT>
+__global__ __launch_bounds__(256) void heavy_sum_w1_kernel(const int32_t* __restrict__ slot_begin,
+                                                           float* __restrict__ slots,
+                                                           const double* __restrict__ yty) {
+  constexpr int CN = 8, NT = kW1NT, NE = (NT * 4 + CN + 1) * 64;
+  const int h = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= NE) return;
+  const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    a0 += (double)slots[(int64_t)s * kW1Slot + e];
+    a1 += (double)slots[(int64_t)(s + 1) * kW1Slot + e];
+    a2 += (double)slots[(int64_t)(s + 2) * kW1Slot + e];
+    a3 += (double)slots[(int64_t)(s + 3) * kW1Slot + e];
+  }
+  for (; s < s1; ++s) a0 += (double)slots[(int64_t)s * kW1Slot + e];
+  double v = (a0 + a1) + (a2 + a3);
+  const int ent = e >> 6;
+  if (IMPLICIT && ent < NT * 4) {
+    const int t = ent >> 2, r = ent & 3, lane = e & 63;
+    const int i = (4 * (lane >> 4) + r) * CN + FullTiles<CN>::l1(t);
+    const int j = (lane & 15) * CN + FullTiles<CN>::l2(t);
+    const int hi = i > j ? i : j, lo = i > j ? j : i;
+    v += yty[hi * (hi + 1) / 2 + lo];
+  }
+  slots[(int64_t)s0 * kW1Slot + e] = (float)v;
+}
+
+// Launch 2b: one wavefront per heavy row solves from its summed slot.
 template <bool IMPLICIT>
 __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
     const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
-    float* __restrict__ X, int ld, int k, float reg,
-    const double* yty,  // not __restrict__: its loads stay inside their entry group
-    int32_t* __restrict__ status) {
+    float* __restrict__ X, int ld, int k, float reg, int32_t* __restrict__ status) {
   constexpr int CN = 8, NT = kW1NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
-  const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
+  const float* sl = slots + (int64_t)slot_begin[h] * kW1Slot + lane;
   floatx4 A[NT];
   float bt[CN];
-  float npos_f = 0.f;
-  static_for<(NT * 4 + CN + 1 + 15) / 16>([&](auto gc) {
-    constexpr int g = decltype(gc)::value;
-    double a[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) a[j] = 0.0;
-    for (int s = s0; s < s1; ++s) {
-      const float* sl = slots + (int64_t)s * kW1Slot + lane;
+  for (int e = 0; e < NT * 4; ++e) A[e / 4][e % 4] = sl[e * 64];
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (16 * g + j < NT * 4 + CN + 1) a[j] += (double)sl[(16 * g + j) * 64];
-    }
-    static_for<16>([&](auto jc) {
-      constexpr int e = 16 * g + decltype(jc)::value;
-      if constexpr (e < NT * 4) {
-        double v = a[decltype(jc)::value];
-        if constexpr (IMPLICIT) {
-          int i, j;
-          tile_ij<8>(FullTiles<8>::l1(e / 4), FullTiles<8>::l2(e / 4), e % 4, i, j);
-          const int hi = i > j ? i : j, lo = i > j ? j : i;
-          v += yty[hi * (hi + 1) / 2 + lo];
-        }
-        A[e / 4][e % 4] = (float)v;
-      } else if constexpr (e < NT * 4 + CN) {
-        bt[e - NT * 4] = (float)a[decltype(jc)::value];
-      } else if constexpr (e == NT * 4 + CN) {
-        npos_f = (float)a[decltype(jc)::value];
-      }
-    });
-    asm volatile("" ::: "memory");
-  });
+  for (int c = 0; c < CN; ++c) bt[c] = sl[(NT * 4 + c) * 64];
+  const float npos_f = sl[(NT * 4 + CN) * 64];
   const int64_t n_reg = IMPLICIT ? (int64_t)npos_f : (row_ptr[row + 1] - row_ptr[row]);
   w1_finish_and_solve<false>(A, 1.f, bt, n_reg, nullptr, smem, k, reg, X + (int64_t)row * ld, ld,
                              row, status);
@@ -2121,6 +2128,25 @@ __global__ __launch_bounds__(256, 3) void reduce_solve_wg_kernel(
 #undef CALL
 }
 
+// Element-wise fp64 sum of the YtY task slots (fixed order: four interleaved
+// partial sums, then combined), so the final reduce reads one slot.
+__global__ __launch_bounds__(256) void slot_sum_kernel(const double* __restrict__ slots,
+                                                       int nslots, int64_t slot_len,
+                                                       double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= slot_len) return;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int i = 0;
+  for (; i + 4 <= nslots; i += 4) {
+    s0 += slots[(int64_t)i * slot_len + e];
+    s1 += slots[(int64_t)(i + 1) * slot_len + e];
+    s2 += slots[(int64_t)(i + 2) * slot_len + e];
+    s3 += slots[(int64_t)(i + 3) * slot_len + e];
+  }
+  for (; i < nslots; ++i) s0 += slots[(int64_t)i * slot_len + e];
+  out[e] = (s0 + s1) + (s2 + s3);
+}
+
 __global__ __launch_bounds__(256, 2) void yty_partial_wg_kernel(const float* __restrict__ Y,
                                                                 int64_t n, int ld, int k,
                                                                 double* __restrict__ slots) {
@@ -2298,10 +2324,13 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                    ld, k, reg, alpha, ytyC, slots_f, status_dev,  \
                                                    scal, Ysp, kp, zero_row);                      \
     ALS_LAUNCH_CHECK();                                                                           \
-    if (g2)                                                                                       \
+    if (g2) {                                                                                     \
+      heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot + 255) / 256, g2), 256, 0, st>>>(                 \
+          heavy_slot_begin, slots_f, yty_packed);                                                 \
+      ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_w1_kernel<IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,      \
-                                                     slots_f, X_dst, ld, k, reg, yty_packed,      \
-                                                     status_dev);                                 \
+                                                     slots_f, X_dst, ld, k, reg, status_dev);     \
+    }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
   } while (0)
   if (implicit) {
@@ -2325,7 +2354,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
 
 size_t als_yty_workspace_bytes(int64_t n, int32_t k) {
   const int64_t nslots = n > 0 ? (n + kYtyChunk - 1) / kYtyChunk : 1;
-  return align_up(sizeof(double) * yty_slot_doubles(k) * (size_t)nslots) + 256;
+  // task slots + their element-wise sum
+  return align_up(sizeof(double) * yty_slot_doubles(k) * (size_t)(nslots + 1)) + 256;
 }
 
 int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed_out, void* ws,
@@ -2346,11 +2376,19 @@ int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed
     ALS_HIP(hipMemsetAsync(yty_packed_out, 0, sizeof(double) * kp * (kp + 1) / 2, st));
     return ALS_OK;
   }
+  const int64_t slen = (int64_t)yty_slot_doubles(k);
+  double* ssum = slots + (int64_t)nslots * slen;
+  auto sum_slots = [&]() -> int {
+    slot_sum_kernel<<<(unsigned)((slen + 255) / 256), 256, 0, st>>>(slots, nslots, slen, ssum);
+    ALS_LAUNCH_CHECK();
+    return ALS_OK;
+  };
 #define ALS_YTY_LAUNCH(CN)                                                                    \
   do {                                                                                        \
     yty_partial_kernel<CN><<<nslots, 64, 0, st>>>(Y, n, ld, k, slots);                        \
     ALS_LAUNCH_CHECK();                                                                       \
-    yty_reduce_kernel<CN><<<1, 64, 0, st>>>(slots, nslots, yty_packed_out);                   \
+    if (sum_slots() != ALS_OK) return ALS_EDEVICE;                                            \
+    yty_reduce_kernel<CN><<<1, 64, 0, st>>>(ssum, 1, yty_packed_out);                         \
     ALS_LAUNCH_CHECK();                                                                       \
   } while (0)
   if (cn == 1) ALS_YTY_LAUNCH(1);
@@ -2359,7 +2397,8 @@ int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed
   else {
     yty_partial_wg_kernel<<<nslots, 256, 0, st>>>(Y, n, ld, k, slots);
     ALS_LAUNCH_CHECK();
-    yty_reduce_wg_kernel<<<1, 256, 0, st>>>(slots, nslots, yty_packed_out);
+    if (sum_slots() != ALS_OK) return ALS_EDEVICE;
+    yty_reduce_wg_kernel<<<1, 256, 0, st>>>(ssum, 1, yty_packed_out);
     ALS_LAUNCH_CHECK();
   }
 #undef ALS_YTY_LAUNCH

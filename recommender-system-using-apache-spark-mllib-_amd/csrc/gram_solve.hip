@@ -377,12 +377,12 @@ __device__ __forceinline__ int split_exponent(float m) {
 }
 
 // Per-step register set of the split Gram: 8 ratings x NC dims of this lane
-// (unscaled), their ratings, and validity via y = 0.
+// (unscaled).  The per-rating weights stay in the LDS staging block until the
+// step is consumed: w = Gram weight (implicit: sc sqrt(alpha |r|)), b = rhs
+// weight (implicit: (1 + alpha |r|) [r > 0]), both 0 for missing ratings.
 template <int NC>
 struct SplitStep {
   float y[8][NC];
-  float r[8];
-  unsigned valid;  // bit j: rating j of this lane's slot exists (else weights 0)
 };
 
 // Stage the (column, rating) pairs of one 64-rating block in LDS (wave-private).
@@ -393,50 +393,61 @@ __device__ __forceinline__ void stage_block(int* __restrict__ st_c, float* __res
   st_r[lane] = rv;
 }
 
+// Split Gram staging: columns, Gram weights and rhs weights of one 64-rating
+// block (computed once per rating here instead of once per lane of its group).
+template <bool IMPLICIT>
+__device__ __forceinline__ void stage_weights(int* __restrict__ st_c, float* __restrict__ st_w,
+                                              float* __restrict__ st_b, int ci, float rv, float sc,
+                                              float alpha) {
+  const int lane = threadIdx.x & 63;
+  const bool v = ci >= 0;
+  float w, b;
+  if constexpr (IMPLICIT) {
+    const float c1 = alpha * fabsf(rv);
+    w = v ? sc * __builtin_sqrtf(c1) : 0.f;
+    b = (v && rv > 0.f) ? 1.f + c1 : 0.f;
+  } else {
+    w = v ? sc : 0.f;
+    b = v ? rv : 0.f;
+  }
+  st_c[lane] = ci;
+  st_w[lane] = w;
+  st_b[lane] = b;
+}
+
 // Issue the gathers of one 32-rating step (half h of the staged block).
 template <int CN, class TS>
 __device__ __forceinline__ void split_issue(SplitStep<TS::NC>& s, const int* __restrict__ st_c,
-                                            const float* __restrict__ st_r, int h,
-                                            const float* __restrict__ Y, int ld, int d0, int k) {
+                                            int h, const float* __restrict__ Y, int ld, int d0,
+                                            int k) {
   const int q = (threadIdx.x & 63) >> 4;
   const int o = 32 * h + 8 * q;
   const int4 c0 = *reinterpret_cast<const int4*>(st_c + o);
   const int4 c1 = *reinterpret_cast<const int4*>(st_c + o + 4);
-  const float4 r0 = *reinterpret_cast<const float4*>(st_r + o);
-  const float4 r1 = *reinterpret_cast<const float4*>(st_r + o + 4);
   const int ids[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-  s.r[0] = r0.x; s.r[1] = r0.y; s.r[2] = r0.z; s.r[3] = r0.w;
-  s.r[4] = r1.x; s.r[5] = r1.y; s.r[6] = r1.z; s.r[7] = r1.w;
-  s.valid = 0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    s.valid |= (ids[j] >= 0 ? 1u : 0u) << j;
+  for (int j = 0; j < 8; ++j)
     TS::load_clamped(Y + (int64_t)(ids[j] >= 0 ? ids[j] : 0) * ld, s.y[j], d0, ld);
-  }
 }
 
 // Consume one step, part 1 (VALU): rhs FMAs and the hi/lo split of w*y.
 template <class TS, bool IMPLICIT>
-__device__ __forceinline__ void split_prepare(const SplitStep<TS::NC>& s, float sc, float alpha,
+__device__ __forceinline__ void split_prepare(const SplitStep<TS::NC>& s,
+                                              const float* __restrict__ st_w,
+                                              const float* __restrict__ st_b, int h,
                                               uint32_t (&hi)[TS::NC][4], uint32_t (&lo)[TS::NC][4],
                                               float (&bf)[TS::NRA]) {
-  float w[8], cb[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const bool v = (s.valid >> j) & 1u;
-    if constexpr (IMPLICIT) {
-      const float c1 = alpha * fabsf(s.r[j]);
-      w[j] = v ? sc * __builtin_sqrtf(c1) : 0.f;
-      cb[j] = (v && s.r[j] > 0.f) ? 1.f + c1 : 0.f;
-    } else {
-      w[j] = v ? sc : 0.f;
-      cb[j] = v ? s.r[j] : 0.f;
-    }
-  }
+  const int o = 32 * h + 8 * ((threadIdx.x & 63) >> 4);
+  const float4 w0 = *reinterpret_cast<const float4*>(st_w + o);
+  const float4 w1 = *reinterpret_cast<const float4*>(st_w + o + 4);
+  const float4 b0 = *reinterpret_cast<const float4*>(st_b + o);
+  const float4 b1 = *reinterpret_cast<const float4*>(st_b + o + 4);
+  const float w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  const float b[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
   for (int c = 0; c < TS::NR; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bf[c] = fmaf(cb[j], s.y[j][c], bf[c]);
+    for (int j = 0; j < 8; ++j) bf[c] = fmaf(b[j], s.y[j][c], bf[c]);
 #pragma unroll
   for (int c = 0; c < TS::NC; ++c)
 #pragma unroll
@@ -472,8 +483,9 @@ __device__ __forceinline__ void gram_accumulate_split(
     floatx4 (&acc)[TS::N], float (&bf)[TS::NRA], int& npos, int* __restrict__ st) {
   const int lane = threadIdx.x & 63, m = lane & 15;
   const int d0 = m * CN;
-  int* st_c = st;
-  float* st_r = reinterpret_cast<float*>(st + 64);
+  int* st_c = st;  // 192 words: columns, Gram weights, rhs weights
+  float* st_w = reinterpret_cast<float*>(st + 64);
+  float* st_b = reinterpret_cast<float*>(st + 128);
   if (pe <= pb) return;
   auto load_idx = [&](int64_t base, int& ci, float& rv) {
     ci = -1;
@@ -487,35 +499,34 @@ __device__ __forceinline__ void gram_accumulate_split(
   const int nsteps = (int)((n + 31) >> 5);
   int ci_n, ci_c;
   float rv_n, rv_c;
-  (void)rv_c;
   load_idx(pb, ci_c, rv_c);
   load_idx(pb + 64, ci_n, rv_n);
-  stage_block(st_c, st_r, ci_c, rv_c);
+  stage_weights<IMPLICIT>(st_c, st_w, st_b, ci_c, rv_c, sc, alpha);
   if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_c >= 0 && rv_c > 0.f));
   wave_lds_sync();
   // One register set for the gathered rows: step s is split into its f16
   // operands, then the gathers of step s+1 are issued into the same registers,
   // then step s's MFMAs run while those loads are in flight.
   SplitStep<TS::NC> sA;
-  split_issue<CN, TS>(sA, st_c, st_r, 0, Y, ld, d0, k);
+  split_issue<CN, TS>(sA, st_c, 0, Y, ld, d0, k);
   // rhs: fp32 partials per lane over 64-rating blocks, summed into bf
   float bp[TS::NRA];
 #pragma unroll
   for (int c = 0; c < TS::NRA; ++c) bp[c] = 0.f;
   for (int s = 0; s < nsteps; ++s) {
     uint32_t hi[TS::NC][4], lo[TS::NC][4];
-    split_prepare<TS, IMPLICIT>(sA, sc, alpha, hi, lo, bp);
+    split_prepare<TS, IMPLICIT>(sA, st_w, st_b, s & 1, hi, lo, bp);
     const int s1 = s + 1;
     if (s1 < nsteps) {
       // step s1 uses block s1>>1, half s1&1; a new block is staged from the
       // pairs prefetched one block earlier
       if ((s1 & 1) == 0) {
-        stage_block(st_c, st_r, ci_n, rv_n);
+        stage_weights<IMPLICIT>(st_c, st_w, st_b, ci_n, rv_n, sc, alpha);
         if constexpr (IMPLICIT) npos += __popcll(__ballot(ci_n >= 0 && rv_n > 0.f));
         wave_lds_sync();
         load_idx(pb + 64 * (int64_t)((s1 >> 1) + 1), ci_n, rv_n);
       }
-      split_issue<CN, TS>(sA, st_c, st_r, s1 & 1, Y, ld, d0, k);
+      split_issue<CN, TS>(sA, st_c, s1 & 1, Y, ld, d0, k);
     }
     split_mfma<TS>(hi, lo, acc);
     if (s & 1) {
@@ -1307,7 +1318,7 @@ struct SmemBytes {
   static constexpr int value = (int)sizeof(float) * PanelLds<CN>::SIZE;
 };
 template <>
-struct SmemBytes<8> {  // W1: transposition buffer (the Gram's 128-word staging fits in it)
+struct SmemBytes<8> {  // W1: transposition buffer (the Gram's 192-word staging fits in it)
   static constexpr int value = (int)sizeof(float) * W1Lds::SIZE;
 };
 
@@ -1994,7 +2005,7 @@ __device__ __forceinline__ void wg_gram_solve_task(
     pb = row_ptr[row];
     pe = row_ptr[row + 1];
   }
-  int* st = reinterpret_cast<int*>(lds) + 128 * R;
+  int* st = reinterpret_cast<int*>(lds) + 192 * R;
   float inv2;
   if constexpr (IMPLICIT) {
     const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));

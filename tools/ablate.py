@@ -67,12 +67,16 @@ def main():
         Ysp, ey = split_table(Y, k)
         er = 14 - math.floor(math.log2(float(blk.val.abs().max())))
         sc = (Y.shape[0], 2.0 ** er, 2.0 ** (-2 * ey), 2.0 ** (-ey - er))
+        col = blk.col
+        if "--local-cols" in sys.argv:
+            # every gather hits the first 64 rows of Y (L2-resident): isolates gather latency
+            col = (blk.col & 63).contiguous()
         for mode in modes:
             times = []
             for rep in range(4):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                rc = fn(mode, blk.row_ptr.data_ptr(), blk.col.data_ptr(),
+                rc = fn(mode, blk.row_ptr.data_ptr(), col.data_ptr(),
                                   blk.val.data_ptr(), blk.light_rows.data_ptr(), blk.n_light,
                                   Ysp.data_ptr(), *sc, X2.data_ptr(), k, 0.1, st.data_ptr(),
                                   torch.cuda.current_stream().cuda_stream)

@@ -7,24 +7,38 @@
 //   computeYtY (implicit)                  (dspr over all src rows + treeAggregate)
 // reached from ALS.train at RecommenderSystem.py:148-149, :163, :218.
 //
-// MI355X design (DESIGN.md §K2/K3):
-//  * One wavefront per task.  A task is a whole "light" row (<= chunk ratings)
-//    or one chunk of a heavy row.  Rows arrive longest-first (LPT schedule).
-//  * Gram on the matrix cores: v_mfma_f32_16x16x4_f32 (exact fp32 products,
-//    k-ordered fp32 fma accumulation).  The MFMA's K dimension is the rating
-//    index: 4 ratings per instruction, lane (q = lane>>4, m = lane&15) holds
-//    factor dims m*CN .. m*CN+CN-1 of rating q, loaded straight from HBM /
-//    Infinity Cache as one float4 (a whole 256-B row per 16 lanes), so the
-//    gather needs no LDS staging.  With that dim permutation the k x k Gram is
-//    CN x CN tiles of 16x16; only the CN(CN+1)/2 upper tiles are computed
-//    (the matrix is symmetric, as Spark's packed dspr exploits).
-//  * fp32 accumulators are flushed into fp64 registers every 64 ratings, so
-//    the Gram error is that of 64-term fp32 sums, independent of row length;
-//    across blocks and across chunks accumulation is fp64 like Spark's.
-//  * The solve never leaves the CU: the regularised Gram is packed (lower) into LDS
-//    (lambda * n on the diagonal, Spark's ALS-WR weighting, added in fp64), then
-//    factored by a row-per-lane LDL^T with the right-hand side carried
-//    as an augmented column, followed by a column-sweep back substitution.
+// MI355X design (DESIGN.md §4 K2/K3):
+//  * A task is a whole "light" row (<= chunk ratings, default 2048) or one
+//    2048-rating chunk of a heavy row; light rows arrive longest-first (LPT).
+//    k <= 64: one wavefront per task (gram_solve_kernel<CN>); 64 < k <= 128: one
+//    wavefront per task with the whole 128 x 128 system in its registers
+//    (gram_solve_w1_kernel, "W1"; gram_solve_wg_kernel = 4-wave alternative,
+//    ALS_K128_PATH=wg).
+//  * Gram on the f16 matrix cores with fp32-grade products: every operand t is
+//    carried as hi = f16_rn(t), lo = f16_rn(t - hi) after a power-of-two scale
+//    (largest |t| in [2^14, 2^15), from max |Y| and max |r| computed on the
+//    device), and each 16 x 16 tile accumulates hi.hi + hi.lo + lo.hi with three
+//    v_mfma_f32_16x16x32_f16 per 32 ratings (~2^-21 relative per product).
+//    MFMA K = rating index; lane (q, m) holds ratings 8q..8q+7 of a step and dims
+//    m*CN .. m*CN+CN-1, so only the CN(CN+1)/2 upper tiles of the dim-permuted
+//    Gram are computed (Spark's packed dspr uses the same symmetry).
+//    Explicit: Y is pre-split once per half-sweep into hi|lo words
+//    (split_table_kernel) and the rhs runs on the matrix cores; implicit: the
+//    fp32 rows are split in registers after the per-rating weight, whose
+//    sqrt(alpha |r|) and (1 + alpha |r|) are computed once per rating when the
+//    64-rating block is staged in LDS.
+//  * Accumulation: fp32 within a task (<= 2048 ratings; test_gpu_configs pins
+//    the error at the production chunk), fp64 across a heavy row's chunks
+//    (partial slots summed element-wise in a fixed order, deterministic).
+//  * Normal equations as CholeskySolver.solve: A_ii += lambda * n (n = #ratings,
+//    implicit: #ratings > 0), implicit YtY merged in fp64 before the one
+//    rounding to fp32; padded dims get identity rows and zero rhs.
+//  * Solve (fp32, same solution as Spark's dppsv): k <= 64 column-per-lane panel
+//    LDL^T with the trailing tiles on fp32 MFMA; W1 block elimination with
+//    16 x 16 diagonal inverses by the sweep operator (VALU, DPP broadcasts) and
+//    the Pm / Schur products on fp32 MFMA (see w1_solve).
+//  * YtY (K2b): 512-row tasks of the same MFMA Gram, fp64 slots, parallel slot
+//    sum, fixed order.
 #include "als_common.h"
 
 #include <algorithm>

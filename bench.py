@@ -389,7 +389,7 @@ def run_single(args):
             out["configs3"], out["configs4"] = big_single(args, dev)
         except Exception as e:  # the primary line must still print
             out["configs3"] = {"error": f"{type(e).__name__}: {e}"[:300]}
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=OUT, flush=True)
 
 
 def _train_triples(core):
@@ -511,11 +511,25 @@ def run_distributed(args):
             if rank == 0:
                 out["configs3"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=OUT, flush=True)
     dist.destroy_process_group()
 
 
+def _json_stdout():
+    """Reserve stdout for the one JSON line: everything else written to fd 1 from here
+    on (RCCL prints its version banner there) goes to stderr."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
+OUT = sys.stdout
+
+
 def main():
+    global OUT
+    OUT = _json_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)

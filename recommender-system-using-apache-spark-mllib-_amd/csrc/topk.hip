@@ -19,17 +19,17 @@
 //
 // Workgroup = 4 wavefronts x RG row groups = 64 RG query rows.  The workgroup
 // sweeps V in tiles double-buffered in LDS (one barrier per tile, the loads of
-// the tile after next in flight).  Per 16 V rows each wave computes RG 16 x 16
-// score blocks, filters them against its rows' current k-th best score and
-// inserts the rare survivors into a sorted list in LDS with a wave-cooperative
-// insertion.  Order: score descending, ties by
-// ascending index (the build's deterministic tie rule).
-// Scores are compared in the scaled domain (exact: powers of two) and
-// unscaled on output.
-//
-// When the split kernel's lists do not fit the LDS, topk_kernel — the same
-// structure with fp32 MFMA (v_mfma_f32_16x16x4_f32) straight from the fp32
-// rows and 64 query rows per workgroup — is used.
+// the tile after next in flight).  V is swept in order of decreasing row norm
+// (bucketed; the high-scoring rows come first, so the lists fill with
+// near-final entries early), each 16 x 16 score block is filtered against its
+// rows' current k-th best score, and the rare survivors are inserted into the
+// per-row lists: in registers for top <= 16, sorted in LDS with a
+// wave-cooperative insertion above.  Insertions compare (score, V row index)
+// exactly, so the sweep order changes the speed, not the result.  Order: score
+// descending, ties by ascending index (the build's deterministic tie rule,
+// SURVEY Appendix A.6).  Scores are compared in the scaled domain (exact:
+// powers of two) and unscaled on output.  An all-zero query row scores 0
+// against every V row; its list is the first `top` rows by index.
 #include "als_common.h"
 
 #include <algorithm>
@@ -89,16 +89,19 @@ __device__ __forceinline__ bool beats(float s1, int i1, float s2, int i2) {
 // row's current k-th (score, index) are inserted one at a time by the whole
 // wave (rank by ballot, shift, insert), lowest lane first.
 __device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_t n_v,
-                                           float (&ts)[4], int (&ti)[4], float* __restrict__ ls,
+                                           const int32_t* __restrict__ bperm, float (&ts)[4],
+                                           int (&ti)[4], float* __restrict__ ls,
                                            int* __restrict__ li, int* __restrict__ len, int slot0,
-                                           int top) {
+                                           int top, unsigned live) {
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  const int vidx = ibase + m;
-  const bool vin = (int64_t)vidx < n_v;
+  const bool vin = (int64_t)(ibase + m) < n_v;
+  // V row index of table row ibase + m (the sweep is norm-ordered; bperm = the
+  // block's slice of the tile's order in LDS)
+  const int vidx = vin ? bperm[m] : 0x7fffffff;
   int pend = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
-    if (vin && beats(acc[r], vidx, ts[r], ti[r])) pend |= 1 << r;
+    if (vin && ((live >> (4 * q + r)) & 1u) && beats(acc[r], vidx, ts[r], ti[r])) pend |= 1 << r;
   uint64_t any = __ballot(pend != 0);
   while (any) {
     const int L = __builtin_ctzll(any);
@@ -107,7 +110,7 @@ __device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_
     const int rL = __builtin_amdgcn_readlane(myr, L);
     const float sc =
         __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mys), L));
-    const int itm = ibase + (L & 15);
+    const int itm = __builtin_amdgcn_readlane(vidx, L);
     const int slot = slot0 + 4 * (L >> 4) + rL;  // list row within the workgroup
     float* lsr = ls + slot * top;
     int* lir = li + slot * top;
@@ -174,14 +177,21 @@ __device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_
 // Write the lists of rows slot0 .. slot0+15 (one wave) to the outputs.
 __device__ __forceinline__ void topk_write(const float* __restrict__ ls, const int* __restrict__ li,
                                            const int* __restrict__ len, int slot0, int64_t qbase,
-                                           int64_t n_q, int top, float unscale,
-                                           int32_t* __restrict__ idx_out,
+                                           int64_t n_q, int64_t n_v, int top, float unscale,
+                                           unsigned live, int32_t* __restrict__ idx_out,
                                            float* __restrict__ score_out) {
   const int lane = threadIdx.x & 63;
   for (int rr = 0; rr < 16; ++rr) {
     const int slot = slot0 + rr;
     const int64_t row = qbase + slot;
     if (row >= n_q) break;
+    if (!((live >> rr) & 1u)) {  // all-zero query row: every score is 0, ties by index
+      for (int e = lane; e < top; e += 64) {
+        idx_out[row * top + e] = e < n_v ? e : -1;
+        score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+      }
+      continue;
+    }
     const int n = len[slot];
     for (int e = lane; e < top; e += 64) {
       idx_out[row * top + e] = e < n ? li[slot * top + e] : -1;
@@ -190,11 +200,95 @@ __device__ __forceinline__ void topk_write(const float* __restrict__ ls, const i
   }
 }
 
-// V -> split planes, row r = [hi(sv v[0..KQ)) | lo(sv v[0..KQ))] (f16), dims >= k zero.
+// Sweep order: V rows by decreasing norm (4096 log-spaced buckets, 128 per octave;
+// order inside a bucket arbitrary).  Large-norm rows carry most top scores, so the
+// lists fill with near-final entries early and later rows rarely pass the filter.
+// The order only affects speed: insertion compares (score, V row index) exactly.
+constexpr int kTkBuckets = 4096;
+
+// 16 lanes per V row: squared norm -> bucket (0 = largest norms).
+__device__ __forceinline__ int tk_row_bucket(const float* __restrict__ V, int64_t r, int ld,
+                                             int k, float log2_ref) {
+  const int l = threadIdx.x & 15;
+  float s = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int d = 4 * l + 64 * h;
+    if (d < k) {
+      const float4 v = *reinterpret_cast<const float4*>(V + r * ld + d);
+      s += v.x * v.x + (d + 1 < k ? v.y * v.y : 0.f) + (d + 2 < k ? v.z * v.z : 0.f) +
+           (d + 3 < k ? v.w * v.w : 0.f);
+    }
+  }
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (!(s > 0.f)) return kTkBuckets - 1;
+  const float b = (log2_ref - 0.5f * __log2f(s)) * 128.f;  // octaves below the reference
+  return b <= 0.f ? 0 : (b >= (float)(kTkBuckets - 1) ? kTkBuckets - 1 : (int)b);
+}
+
+__device__ __forceinline__ float tk_log2_ref(const float* __restrict__ scal, int k) {
+  // reference norm: max |v| * sqrt(k) bounds every row norm
+  return __log2f(fmaxf(scal[1], 1e-30f)) + 0.5f * __log2f((float)k);
+}
+
+__global__ __launch_bounds__(256) void tk_bucket_hist_kernel(const float* __restrict__ V,
+                                                             int64_t n_v, int ld, int k,
+                                                             const float* __restrict__ scal,
+                                                             int32_t* __restrict__ hist) {
+  const float ref = tk_log2_ref(scal, k);
+  for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; r < n_v;
+       r += ((int64_t)gridDim.x * 256) >> 4) {
+    const int b = tk_row_bucket(V, r, ld, k, ref);
+    if ((threadIdx.x & 15) == 0) atomicAdd(hist + b, 1);
+  }
+}
+
+// Exclusive scan of the bucket counts (one workgroup) -> scatter cursors.
+__global__ __launch_bounds__(1024) void tk_bucket_scan_kernel(int32_t* __restrict__ hist) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  int v[4], s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = hist[4 * t + j];
+    s += v[j];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int x = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hist[4 * t + j] = run;
+    run += v[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void tk_bucket_scatter_kernel(const float* __restrict__ V,
+                                                                int64_t n_v, int ld, int k,
+                                                                const float* __restrict__ scal,
+                                                                int32_t* __restrict__ cursor,
+                                                                int32_t* __restrict__ perm) {
+  const float ref = tk_log2_ref(scal, k);
+  for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; r < n_v;
+       r += ((int64_t)gridDim.x * 256) >> 4) {
+    const int b = tk_row_bucket(V, r, ld, k, ref);
+    if ((threadIdx.x & 15) == 0) perm[atomicAdd(cursor + b, 1)] = (int32_t)r;
+  }
+}
+
+// V -> split planes in sweep order, table row t = V row perm[t]:
+// [hi(sv v[0..KQ)) | lo(sv v[0..KQ))] (f16), dims >= k zero.
 __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __restrict__ V,
                                                                int64_t n_v, int ld, int k,
                                                                int kq_shift,
                                                                const float* __restrict__ scal,
+                                                               const int32_t* __restrict__ perm,
                                                                _Float16* __restrict__ out) {
   const float sv = ldexpf(1.f, tk_split_exponent(scal[1]));
   const int kq = 1 << kq_shift;
@@ -203,7 +297,7 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
        e += (int64_t)gridDim.x * 256) {
     const int64_t r = e >> kq_shift;
     const int d = (int)(e & (kq - 1));
-    const float t = d < k ? sv * V[r * ld + d] : 0.f;
+    const float t = d < k ? sv * V[(int64_t)perm[r] * ld + d] : 0.f;
     _Float16 h, l;
     tk_split(t, h, l);
     out[2 * (r << kq_shift) + d] = h;
@@ -241,16 +335,14 @@ __host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
 
 // Insert candidate (sc, id) into a list sorted by ascending goodness (k-th best at
 // [0]; entries past `top` are sentinels (+inf, -1) that nothing beats; unfilled
-// entries are (-inf, INT_MAX)).  Every list index is below `id` (V is swept in
-// index order), so the candidate beats entry j iff sc > its score or the entry
-// is unfilled.  c_j is monotone (true for j < p); the list becomes
-// [.. entries 1..p-1, candidate, entries p..]: independent selects, no chain.
-// The caller has checked that the candidate beats [0] and is not NaN.
+// entries are (-inf, INT_MAX)).  c_j = candidate beats entry j is monotone (true
+// for j < p); the list becomes [.. entries 1..p-1, candidate, entries p..]:
+// independent selects, no chain.  The caller has checked that it beats [0].
 template <int TOPR>
 __device__ __forceinline__ void tk_insert(float (&sv)[TOPR], int (&iv)[TOPR], float sc, int id) {
   bool c[TOPR + 1];
 #pragma unroll
-  for (int j = 0; j < TOPR; ++j) c[j] = sc > sv[j] || iv[j] == 0x7fffffff;
+  for (int j = 0; j < TOPR; ++j) c[j] = beats(sc, id, sv[j], iv[j]);
   c[TOPR] = false;
 #pragma unroll
   for (int j = 0; j < TOPR; ++j) {
@@ -268,6 +360,7 @@ __device__ __forceinline__ void tk_insert(float (&sv)[TOPR], int (&iv)[TOPR], fl
 template <int NK, int RG, int TOPR, int MODE = 0>
 __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
+                                                         const int32_t* __restrict__ perm,
                                                          int64_t n_v, int ld, int k, int top,
                                                          const float* __restrict__ scal,
                                                          int32_t* __restrict__ idx_out,
@@ -281,9 +374,10 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   static_assert(PER * 256 == VT * RW, "tile staging");
   extern __shared__ uint4 smem_u4[];
   uint4* tiles = smem_u4;                                     // [2][VT][RS]
+  int* tperm = reinterpret_cast<int*>(tiles + 2 * VT * RS);   // [2][VT] V row of each tile row
   // TOPR == 0: [64 RG rows][top] scores, indices, [64 RG] lengths
   // TOPR > 0: per wave and group a 16 x 16 score block [item m][row]
-  float* ls = reinterpret_cast<float*>(tiles + 2 * VT * RS);
+  float* ls = reinterpret_cast<float*>(tperm + 2 * VT);
   int* li = reinterpret_cast<int*>(ls + 64 * RG * top);
   int* len = li + 64 * RG * top;
   float* sblk = ls;
@@ -296,31 +390,40 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   // A operands: group g, k-step s, lane (q, m): dims 32s + 8q .. +7 of query row
   // qbase + 64g + 16w + m, as hi and lo halves.
   tk_half8 ah[RG][NK], al[RG][NK];
+  // live[g] bit rho: query row 16w + rho of group g exists and is not all zero (an
+  // all-zero row scores 0 everywhere: its list is the first `top` rows, written at
+  // the end; it would otherwise tie with every threshold)
+  unsigned live[RG];
 #pragma unroll
   for (int g = 0; g < RG; ++g) {
     const int64_t row = qbase + 64 * g + 16 * w + m;
     const bool ok = row < n_q;
+    bool nz = false;
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int d = 32 * s + 8 * q + j;
         const float t = (ok && d < k) ? su * Q[row * ld + d] : 0.f;
+        nz = nz || t != 0.f;
         _Float16 h, l;
         tk_split(t, h, l);
         ah[g][s][j] = h;
         al[g][s][j] = l;
       }
     }
+    const uint64_t b = __ballot(nz);
+    live[g] = (unsigned)((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFu);
   }
   if (TOPR == 0 && threadIdx.x < 64 * RG) len[threadIdx.x] = 0;
   float ts[RG][4];
   int ti[RG][4];
+  // dead rows (absent or all-zero) keep an unbeatable threshold
 #pragma unroll
   for (int g = 0; g < RG; ++g)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      ts[g][r] = -__builtin_inff();
+      ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? -__builtin_inff() : __builtin_inff();
       ti[g][r] = 0x7fffffff;
     }
   bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
@@ -335,6 +438,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   }
 
   uint4 pre[PER];
+  int pre_p = 0x7fffffff;
   auto fetch = [&](int64_t vb) {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
@@ -342,6 +446,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       const int64_t vrow = vb + x / RW;
       pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW] : make_uint4(0u, 0u, 0u, 0u);
     }
+    if (threadIdx.x < VT) pre_p = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
   };
   auto stage = [&](int buf) {
     uint4* t = tiles + buf * VT * RS;
@@ -350,6 +455,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       const int x = threadIdx.x + 256 * e;
       t[(x / RW) * RS + x % RW] = pre[e];
     }
+    if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p;
   };
   auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {
     // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m
@@ -369,7 +475,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   };
   float sink = 0.f;
   int n_offer = 0;
-  auto filter = [&](const floatx4 (&acc)[RG], int64_t ibase) {
+  auto filter = [&](const floatx4 (&acc)[RG], int64_t ibase, const int* bperm) {
     // acc[g][r] = scaled score(row 64g + 16w + 4q + r, V row ibase + m)
     if constexpr (MODE == 1) {
 #pragma unroll
@@ -378,15 +484,16 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     }
     const bool vin = ibase + m < n_v;
     if constexpr (TOPR > 0) {
-      // full lists: strict > (a tie at the k-th score has a larger index); until
-      // then every block goes to the owner lanes (exact beats() there)
+      // score >= the row's k-th score (a tie may still win on the index: the
+      // owner lanes decide with beats()); until the lists are full every block
+      // goes to the owners
       bool pr[RG][4];
       bool anyl = false;
 #pragma unroll
       for (int g = 0; g < RG; ++g)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          pr[g][r] = vin && (!full || acc[g][r] > (MODE == 2 ? 3.0e38f : ts[g][r]));
+          pr[g][r] = vin && (!full || acc[g][r] >= (MODE == 2 ? 3.0e38f : ts[g][r]));
           anyl = anyl || pr[g][r];
         }
       if (__ballot(anyl) == 0) return;
@@ -412,7 +519,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           const int mm = __builtin_ctz(msk);
           msk &= msk - 1;
           const float sc = sg[16 * mm];
-          const int id = (int)ibase + mm;
+          const int id = bperm[mm];
           if (beats(sc, id, lsv[0], liv[0])) tk_insert<NR>(lsv, liv, sc, id);
         }
         thr[lane] = lsv[0];
@@ -421,26 +528,34 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
         const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
-        ts[g][0] = t4[0]; ts[g][1] = t4[1]; ts[g][2] = t4[2]; ts[g][3] = t4[3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? t4[r] : __builtin_inff();
       }
-      if (!full) full = __ballot(lane < 16 * RG && liv[0] == 0x7fffffff) == 0;
+      if (!full) {
+        const bool open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
+                               liv[0] == 0x7fffffff;
+        full = __ballot(open_list) == 0;
+      }
       return;
     }
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
       bool hit = !full;
       if (full) {
-        const bool p = vin && (acc[g][0] > ts[g][0] || acc[g][1] > ts[g][1] ||
-                               acc[g][2] > ts[g][2] || acc[g][3] > ts[g][3]);
+        const bool p = vin && (acc[g][0] >= ts[g][0] || acc[g][1] >= ts[g][1] ||
+                               acc[g][2] >= ts[g][2] || acc[g][3] >= ts[g][3]);
         hit = __ballot(p) != 0;
       }
       if constexpr (MODE == 3) n_offer += hit ? 1 : 0;
       if (hit)
-        topk_offer(acc[g], (int)ibase, n_v, ts[g], ti[g], ls, li, len, 64 * g + 16 * w, top);
+        topk_offer(acc[g], (int)ibase, n_v, bperm, ts[g], ti[g], ls, li, len, 64 * g + 16 * w,
+                   top, live[g]);
     }
     if (!full) {
       bool f = true;
-      if (lane < 16 * RG) f = len[64 * (lane >> 4) + 16 * w + (lane & 15)] >= top;
+      if (lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u))
+        f = len[64 * (lane >> 4) + 16 * w + (lane & 15)] >= top;
       full = __ballot(!f) == 0;
     }
   };
@@ -459,10 +574,10 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       // issue block c+1's MFMAs, then filter block c
       if (c % 2 == 0) {
         if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc1);
-        filter(acc0, vb + 16 * c);
+        filter(acc0, vb + 16 * c, tperm + buf * VT + 16 * c);
       } else {
         if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc0);
-        filter(acc1, vb + 16 * c);
+        filter(acc1, vb + 16 * c, tperm + buf * VT + 16 * c);
       }
     }
     if (vb + VT < n_v) stage(buf ^ 1);
@@ -477,13 +592,20 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   if constexpr (TOPR > 0) {
     if (lane < 16 * RG) {
       const int64_t row = qbase + 64 * (lane >> 4) + 16 * w + (lane & 15);
+      const bool zero = !((live[lane >> 4] >> (lane & 15)) & 1u);
       if (row < n_q) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
           if (j < top) {
-            const bool real = liv[j] != 0x7fffffff;
-            idx_out[row * top + (top - 1 - j)] = real ? liv[j] : -1;
-            score_out[row * top + (top - 1 - j)] = real ? lsv[j] * unscale : -__builtin_inff();
+            const int e = top - 1 - j;
+            if (zero) {  // every score 0: the first `top` rows, ties by index
+              idx_out[row * top + e] = e < n_v ? e : -1;
+              score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+            } else {
+              const bool real = liv[j] != 0x7fffffff;
+              idx_out[row * top + e] = real ? liv[j] : -1;
+              score_out[row * top + e] = real ? lsv[j] * unscale : -__builtin_inff();
+            }
           }
         }
       }
@@ -492,91 +614,8 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   }
 #pragma unroll
   for (int g = 0; g < RG; ++g)
-    topk_write(ls, li, len, 64 * g + 16 * w, qbase, n_q, top, unscale, idx_out, score_out);
-}
-
-// fp32 scores (used when the split kernel's lists do not fit the LDS).
-template <int CN>
-__global__ __launch_bounds__(256) void topk_kernel(const float* __restrict__ Q, int64_t n_q,
-                                                   const float* __restrict__ V, int64_t n_v,
-                                                   int ld, int k, int top,
-                                                   int32_t* __restrict__ idx_out,
-                                                   float* __restrict__ score_out) {
-  constexpr int KP = 16 * CN;
-  constexpr int KS = KP / 4;      // MFMA k-steps; lane q covers dims [q*KS, q*KS+KS)
-  constexpr int TS = KP + 4;      // padded tile row stride (floats)
-  extern __shared__ float4 smem4[];
-  float* tile = reinterpret_cast<float*>(smem4);        // [64][TS]
-  float* ls = tile + 64 * TS;                           // [64 rows][top] scores
-  int* li = reinterpret_cast<int*>(ls + 64 * top);      // [64 rows][top] indices
-  int* len = li + 64 * top;                             // [64]
-
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  const int64_t qbase = (int64_t)blockIdx.x * 64;
-
-  // A operand (query rows): lane (m, q) holds dims q*KS + s of row qbase + 16w + m.
-  float qa[KS];
-  {
-    const int64_t row = qbase + 16 * w + m;
-    const bool ok = row < n_q;
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int d = q * KS + s;
-      qa[s] = (ok && d < k) ? Q[row * ld + d] : 0.f;
-    }
-  }
-  if (threadIdx.x < 64) len[threadIdx.x] = 0;
-  // per-lane thresholds of its 4 rows (16w + 4q + r)
-  float ts[4];
-  int ti[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    ts[r] = -__builtin_inff();
-    ti[r] = 0x7fffffff;
-  }
-
-  for (int64_t vb = 0; vb < n_v; vb += 64) {
-    __syncthreads();
-    // stage 64 V rows x KP dims (float4 granules), masked beyond n_v / k
-    for (int e = threadIdx.x; e < 64 * (KP / 4); e += 256) {
-      const int rr = e / (KP / 4), c4 = e % (KP / 4);
-      const int64_t vrow = vb + rr;
-      const int d = 4 * c4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (vrow < n_v && d < k) {
-        v = *reinterpret_cast<const float4*>(V + vrow * ld + d);
-        if (d + 1 >= k) v.y = 0.f;
-        if (d + 2 >= k) v.z = 0.f;
-        if (d + 3 >= k) v.w = 0.f;
-      }
-      *reinterpret_cast<float4*>(tile + rr * TS + d) = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      // B operand: lane (m, q) holds dims q*KS + s of V row vb + 16c + m
-      const float* tb = tile + (16 * c + m) * TS + q * KS;
-      floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s4 = 0; s4 < KS; s4 += 4) {
-        const float4 b4 = *reinterpret_cast<const float4*>(tb + s4);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s4 + 0], b4.x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s4 + 1], b4.y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s4 + 2], b4.z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s4 + 3], b4.w, acc, 0, 0, 0);
-      }
-      // acc[r] = score(row 16w + 4q + r, V row vb + 16c + m)
-      topk_offer(acc, (int)(vb + 16 * c), n_v, ts, ti, ls, li, len, 16 * w, top);
-    }
-  }
-  __syncthreads();
-  topk_write(ls, li, len, 16 * w, qbase, n_q, top, 1.f, idx_out, score_out);
-}
-
-static size_t topk_lds_bytes(int cn, int top) {
-  const int kp = 16 * cn;
-  return sizeof(float) * 64 * (kp + 4) + (sizeof(float) + sizeof(int)) * 64 * (size_t)top +
-         sizeof(int) * 64;
+    topk_write(ls, li, len, 64 * g + 16 * w, qbase, n_q, n_v, top, unscale, live[g], idx_out,
+               score_out);
 }
 
 static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
@@ -585,7 +624,7 @@ constexpr int kTopR = 16;  // register-resident lists for top <= kTopR
 
 static size_t topk_split_lds_bytes(int kq, int rg, int top) {
   const int nk = kq / 32;
-  const size_t tiles = 16 * 2 * (size_t)tk_vt(nk) * (size_t)(kq / 4 + 2);
+  const size_t tiles = 16 * 2 * (size_t)tk_vt(nk) * (size_t)(kq / 4 + 2) + 4 * 2 * (size_t)tk_vt(nk);
   if (top <= kTopR) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
   return tiles + (sizeof(float) + sizeof(int)) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
@@ -605,11 +644,17 @@ using namespace als;
 
 extern "C" {
 
+static size_t tk_table_bytes(int64_t n_v, int32_t k) {
+  return align_up(4 * (size_t)topk_kq(k) * (size_t)(n_v > 0 ? n_v : 0));
+}
+
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top) {
   (void)n_q;
   (void)top;
-  // 256 B of scale words, then the split planes of V (2 x KQ halves per row)
-  return 256 + align_up(4 * (size_t)topk_kq(k) * (size_t)(n_v > 0 ? n_v : 0));
+  // 256 B of scale words | split planes of V in sweep order (2 x KQ halves per row) |
+  // sweep order (int32 per V row) | bucket counts / cursors
+  return 256 + tk_table_bytes(n_v, k) + align_up(4 * (size_t)(n_v > 0 ? n_v : 0)) +
+         align_up(4 * (size_t)kTkBuckets);
 }
 
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t ld, int32_t k,
@@ -624,27 +669,9 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   if (n_q == 0) return ALS_OK;
   ALS_REQUIRE(Q && V && idx_out && score_out, ALS_EINVAL, "als_topk: null pointer");
   hipStream_t st = as_stream(stream);
-  const int cn = k <= 16 ? 1 : (k <= 32 ? 2 : (k <= 64 ? 4 : 8));
   const int rg = topk_split_rg(k, top);
-  if (rg == 0) {
-    const size_t lds = topk_lds_bytes(cn, top);
-    ALS_REQUIRE(lds <= kLdsBytes, ALS_EUNSUPPORTED,
-                "als_topk: top %d at rank %d needs %zu B of LDS (> %d)", top, k, lds, kLdsBytes);
-    const unsigned grid = (unsigned)((n_q + 63) / 64);
-#define ALS_TOPK_LAUNCH(CN)                                                                   \
-  do {                                                                                        \
-    ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_kernel<CN>),              \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));       \
-    topk_kernel<CN><<<grid, 256, lds, st>>>(Q, n_q, V, n_v, ld, k, top, idx_out, score_out);  \
-    ALS_LAUNCH_CHECK();                                                                       \
-  } while (0)
-    if (cn == 1) ALS_TOPK_LAUNCH(1);
-    else if (cn == 2) ALS_TOPK_LAUNCH(2);
-    else if (cn == 4) ALS_TOPK_LAUNCH(4);
-    else ALS_TOPK_LAUNCH(8);
-#undef ALS_TOPK_LAUNCH
-    return ALS_OK;
-  }
+  ALS_REQUIRE(rg > 0, ALS_EUNSUPPORTED, "als_topk: top %d at rank %d does not fit the LDS", top,
+              k);
   ALS_REQUIRE(ws != nullptr && ws_bytes >= als_topk_workspace_bytes(n_q, n_v, k, top),
               ALS_EWORKSPACE, "als_topk: workspace %zu < %zu", ws_bytes,
               als_topk_workspace_bytes(n_q, n_v, k, top));
@@ -653,6 +680,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   unsigned* scal_u = static_cast<unsigned*>(ws);
   const float* scal = reinterpret_cast<const float*>(scal_u);
   _Float16* vsp = reinterpret_cast<_Float16*>(static_cast<char*>(ws) + 256);
+  int32_t* perm = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + 256 + tk_table_bytes(n_v, k));
+  int32_t* hist = perm + align_up(4 * (size_t)n_v) / 4;
   const int kq = topk_kq(k);
   const int kq_shift = __builtin_ctz(kq);
   ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
@@ -664,9 +693,18 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     tk_absmax_kernel<<<(int)std::min<int64_t>(1024, (nv_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
         V, nv_el, scal_u + 1);
     ALS_LAUNCH_CHECK();
+    // sweep order: V rows by decreasing norm (bucketed)
+    ALS_HIP(hipMemsetAsync(hist, 0, sizeof(int32_t) * kTkBuckets, st));
+    const int gb = (int)std::min<int64_t>(4096, (n_v * 16 + 255) / 256);
+    tk_bucket_hist_kernel<<<gb, 256, 0, st>>>(V, n_v, ld, k, scal, hist);
+    ALS_LAUNCH_CHECK();
+    tk_bucket_scan_kernel<<<1, 1024, 0, st>>>(hist);
+    ALS_LAUNCH_CHECK();
+    tk_bucket_scatter_kernel<<<gb, 256, 0, st>>>(V, n_v, ld, k, scal, hist, perm);
+    ALS_LAUNCH_CHECK();
     const int64_t total = n_v << kq_shift;
     topk_split_table_kernel<<<(int)std::min<int64_t>(4096, (total + 255) / 256), 256, 0, st>>>(
-        V, n_v, ld, k, kq_shift, scal, vsp);
+        V, n_v, ld, k, kq_shift, scal, perm, vsp);
     ALS_LAUNCH_CHECK();
   }
   const size_t lds = topk_split_lds_bytes(kq, rg, top);
@@ -676,8 +714,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   do {                                                                                          \
     ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, TR>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
-    topk_split_kernel<NK, RG, TR><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, scal,  \
-                                                          idx_out, score_out);                  \
+    topk_split_kernel<NK, RG, TR><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld, k, top,  \
+                                                          scal, idx_out, score_out);            \
     ALS_LAUNCH_CHECK();                                                                         \
   } while (0)
 #define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                 \

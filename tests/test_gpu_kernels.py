@@ -377,6 +377,43 @@ def test_topk_many_tiles_ties_across_tiles(rank, n_v):
     assert any(a in idx[r_] and b in idx[r_] for r_ in range(n_q) for a, b in pairs)
 
 
+@pytest.mark.parametrize("rank,top", [(64, 10), (128, 10), (32, 40)])
+def test_topk_zero_rows_and_norm_order_ties(rank, top):
+    """The sweep visits V by decreasing norm: ties between equal rows far apart in index
+    (the large-norm copy visited first) must still resolve to the lower index; all-zero
+    query rows list the first `top` items with score 0; zero V rows score 0."""
+    rng = np.random.default_rng(rank + top)
+    n_q, n_v = 300, 5000
+    Q = rng.standard_normal((n_q, rank)).astype(np.float32)
+    Q[[0, 7, 299]] = 0.0
+    Vm = (rng.standard_normal((n_v, rank)) * rng.uniform(0.1, 3.0, (n_v, 1))).astype(np.float32)
+    Vm[100:140] = 0.0
+    big = np.argsort(-np.linalg.norm(Vm, axis=1))[:30]  # strong rows, copied to lower indices
+    for t, b in enumerate(big):
+        Vm[t] = Vm[b]
+    ld = E.ld_for(rank)
+    Qd = torch.zeros((n_q, ld), device=DEV)
+    Qd[:, :rank] = torch.as_tensor(Q).to(DEV)
+    Vd = torch.zeros((n_v, ld), device=DEV)
+    Vd[:, :rank] = torch.as_tensor(Vm).to(DEV)
+    idx, sc = E.topk_rows(Qd, n_q, Vd, n_v, rank, top)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    ref_i, ref_s = O.topk(Q, Vm, top)
+    S = Q.astype(np.float64) @ Vm.astype(np.float64).T
+    for row in range(n_q):
+        if not np.array_equal(idx[row], ref_i[row]):
+            bad = np.nonzero(idx[row] != ref_i[row])[0]
+            for p_ in bad:
+                assert abs(S[row, idx[row, p_]] - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
+        np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
+        lst = list(idx[row])
+        for t, b in enumerate(big):  # exact copies: the lower index first
+            if t in lst and b in lst:
+                assert lst.index(t) < lst.index(b)
+    for row in (0, 7, 299):
+        assert list(idx[row]) == list(range(top)) and np.all(sc[row] == 0)
+
+
 def test_topk_fewer_items_than_top():
     Q = torch.randn(70, 8, device=DEV)
     Vm = torch.randn(5, 8, device=DEV)

@@ -21,18 +21,20 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
   const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
   const float* scal = reinterpret_cast<const float*>(ws);
   const uint4* vsp4 = reinterpret_cast<const uint4*>(static_cast<char*>(ws) + 256);
+  const int32_t* perm =
+      reinterpret_cast<const int32_t*>(static_cast<char*>(ws) + 256 + tk_table_bytes(n_v, k));
 #define L(NK, RG, M)                                                                          \
   do {                                                                                        \
     if (top <= kTopR) {                                                                       \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, kTopR, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, \
-                                                                  scal, idx, dbg);            \
+      topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,  \
+                                                                  k, top, scal, idx, dbg);    \
     } else {                                                                                  \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, 0, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, 0, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, n_v, ld, k, top, \
-                                                              scal, idx, dbg);                \
+      topk_split_kernel<NK, RG, 0, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld, k, \
+                                                              top, scal, idx, dbg);           \
     }                                                                                         \
   } while (0)
 #define LM(NK, RG) \

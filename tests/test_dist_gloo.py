@@ -293,3 +293,70 @@ def test_checkpoint_resume_across_world_sizes(tmp_path):
     at = np.load(tmp_path / "at_w2.npz")
     np.testing.assert_array_equal(at["U"], ck)
     np.testing.assert_array_equal(at["V"], np.load(tmp_path / "ckpt" / "item_factors.npy"))
+
+
+def _surface_worker(rank, world, port, out_dir):
+    """ml.ALS.fit / transform / recommendForAllUsers and mllib ALS.train / predictAll on
+    this rank's partition, through make_engine -> ShardedALS (kernels: the oracle)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    import pandas as pd
+    from als_mi355x import distributed as Dm
+    from als_mi355x import engine as Em
+    from als_mi355x.ml.recommendation import ALS as MLALS
+    from als_mi355x.mllib.recommendation import ALS as MLlibALS
+    Dm.HipKernels = lambda device, chunk=None: OracleKernels()  # no GPU here
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r = planted(80, 60, density=0.12, seed=51, heavy_items=(1,))
+    sel = np.arange(len(u)) % world == rank
+    df = pd.DataFrame({"user": u[sel], "item": i[sel], "rating": r[sel]})
+    model = MLALS(rank=4, maxIter=3, regParam=0.1, seed=13).fit(df)
+    assert isinstance(model.engine, Dm.ShardedALS)
+    test = pd.DataFrame({"user": [u[0], u[1], 999], "item": [i[0], i[1], i[2]]})
+    pred = model.transform(test)["prediction"].to_numpy()
+    recs = model.recommendForAllUsers(5)
+    ml_users = recs["user"].to_numpy()
+    ml_items = np.array([[x[0] for x in row] for row in recs["recommendations"]])
+    mm = MLlibALS.train(np.stack([u[sel], i[sel], r[sel]], 1), 4, iterations=3, lambda_=0.1,
+                        seed=13)
+    assert isinstance(mm.engine, Dm.ShardedALS)
+    pa = mm.predictAll([(int(u[2]), int(i[2])), (999, int(i[0]))])
+    assert Em.make_engine is not None
+    np.savez(os.path.join(out_dir, f"surface_{rank}.npz"), pred=pred, users=ml_users,
+             items=ml_items, pa=np.array([[p[0], p[1], p[2]] for p in pa], dtype=np.float64))
+    dist.destroy_process_group()
+
+
+def test_ml_and_mllib_surface_on_sharded_engine(tmp_path):
+    """With a process group of world size 2 initialised, ml/mllib fit builds the
+    sharded engine; predictions, recommendForAllUsers (each rank its own users) and
+    predictAll match a single-process oracle fit from the same seeded start."""
+    world = 2
+    mp.spawn(_surface_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    from oracle import als_oracle as O
+    u, i, r = planted(80, 60, density=0.12, seed=51, heavy_items=(1,))
+    n_users = len(np.unique(u))
+    g = torch.Generator(device="cpu")
+    g.manual_seed(13)
+    x = torch.randn((n_users, 4), generator=g, dtype=torch.float32)
+    U0 = (x / torch.linalg.vector_norm(x, dim=1, keepdim=True)).numpy()
+    U, V, umap, imap, uids, iids = O.train(u, i, r, 4, 3, 0.1, U0=U0)
+    ref_pred = [float(U[umap[u[0]]] @ V[imap[i[0]]]), float(U[umap[u[1]]] @ V[imap[i[1]]])]
+    parts = [np.load(tmp_path / f"surface_{w}.npz") for w in range(world)]
+    ref_i, _ = O.topk(U, V, 5)
+    for d in parts:
+        np.testing.assert_allclose(d["pred"][:2], ref_pred, rtol=1e-5, atol=1e-6)
+        assert np.isnan(d["pred"][2])
+        assert len(d["pa"]) == 1 and d["pa"][0][0] == u[2] and d["pa"][0][1] == i[2]
+        np.testing.assert_allclose(d["pa"][0][2], U[umap[u[2]]] @ V[imap[i[2]]], rtol=1e-5)
+    users = np.concatenate([d["users"] for d in parts])
+    items = np.concatenate([d["items"] for d in parts])
+    np.testing.assert_array_equal(np.sort(users), uids)
+    order = np.argsort(users)
+    np.testing.assert_array_equal(items[order], iids[ref_i])

@@ -1069,15 +1069,19 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
 // rhs layouts: "column" = lane m (any q) holds element m of a 16-block;
 // "row" = lanes of row-group q hold elements 4q..4q+3.
 // ---------------------------------------------------------------------------
-struct W1Lds {
+template <int NB>
+struct W1LdsT {
   static constexpr int CS = 20;                     // floats per column (16 + pad, 16-B aligned)
-  // transposition buffer | rhs vector | Pm tiles of the back substitution (28 x 256)
-  static constexpr int COL = 0, VEC = 16 * CS, PM = VEC + 16, SIZE = PM + 28 * 256;
+  // transposition buffer | rhs vector | Pm tiles of the back substitution (NB(NB-1)/2 x 256)
+  static constexpr int COL = 0, VEC = 16 * CS, PM = VEC + 16,
+                       SIZE = PM + NB * (NB - 1) / 2 * 256;
 };
 
 constexpr int kW1NB = 8;
+using W1Lds = W1LdsT<kW1NB>;
 
-__host__ __device__ constexpr int w1_tile(int i, int j) { return tile_index(kW1NB, i, j); }
+template <int NB>
+__host__ __device__ constexpr int w1_tile(int i, int j) { return tile_index(NB, i, j); }
 
 // v on lanes with (lane & 15) == P, else w (mask from the scalar unit).
 template <int P>
@@ -1191,27 +1195,31 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook) {
 }
 
 // Schur tiles of step K, I-major: u = 0 is (K+1, K+1), the next pivot block.
-__host__ __device__ constexpr int schur_n(int K) { return (7 - K) * (8 - K) / 2; }
+template <int NB>
+__host__ __device__ constexpr int schur_n(int K) { return (NB - 1 - K) * (NB - K) / 2; }
+template <int NB>
 __host__ __device__ constexpr int schur_I(int K, int u) {
   int I = K + 1;
-  while (u >= 8 - I) { u -= 8 - I; ++I; }
+  while (u >= NB - I) { u -= NB - I; ++I; }
   return I;
 }
+template <int NB>
 __host__ __device__ constexpr int schur_J(int K, int u) {
   int I = K + 1;
-  while (u >= 8 - I) { u -= 8 - I; ++I; }
+  while (u >= NB - I) { u -= NB - I; ++I; }
   return I + u;
 }
 
-template <int NT>
-__device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
+// NB = 8 (rank 65-128, W1 kernels) or 4 (rank 33-64, explicit gram_solve_kernel).
+template <int NB>
+__device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
                                          float* __restrict__ lds, int k,
                                          float* __restrict__ xrow, int ld) {
-  static_assert(NT == kW1NB * (kW1NB + 1) / 2, "36 upper tiles");
-  constexpr int NB = kW1NB, CS = W1Lds::CS;
+  using L = W1LdsT<NB>;
+  constexpr int CS = L::CS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  float* col = lds + W1Lds::COL;
-  float* vec = lds + W1Lds::VEC;
+  float* col = lds + L::COL;
+  float* vec = lds + L::VEC;
   float zcol[NB];
   float dmin = 3.0e38f;
   // bcol[J] for J > 0 holds per-row-group partial sums (summed over the groups when
@@ -1223,7 +1231,7 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
   floatx4 Gm, bk;
   auto pivot_block = [&](auto Kc, auto&& hook) {
     constexpr int K = decltype(Kc)::value;
-    *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile(K, K)];
+    *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile<NB>(K, K)];
     wave_lds_order();
     float R[16];
 #pragma unroll
@@ -1248,13 +1256,13 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
   };
   auto schur = [&](auto Kc, auto uc, const floatx4 (&Pm)[NB]) {
     constexpr int K = decltype(Kc)::value, u = decltype(uc)::value;
-    constexpr int I = schur_I(K, u), J = schur_J(K, u);
-    floatx4 acc = A[w1_tile(I, J)];
+    constexpr int I = schur_I<NB>(K, u), J = schur_J<NB>(K, u);
+    floatx4 acc = A[w1_tile<NB>(I, J)];
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[w1_tile(K, I)][s4], Pm[J - K - 1][s4], acc, 0,
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[w1_tile<NB>(K, I)][s4], Pm[J - K - 1][s4], acc, 0,
                                                   0, 0);
-    A[w1_tile(I, J)] = acc;
+    A[w1_tile<NB>(I, J)] = acc;
   };
   pivot_block(std::integral_constant<int, 0>{}, [](auto) {});
   static_for<NB>([&](auto Kc) {
@@ -1269,14 +1277,14 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
         floatx4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Gm[s4], A[w1_tile(K, J)][s4], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Gm[s4], A[w1_tile<NB>(K, J)][s4], acc, 0, 0, 0);
         Pm[decltype(jc)::value] = acc;
         bcol[J] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
       });
       // Pm of block row K -> LDS for the back substitution (lane-private slots)
       static_for<NB - 1 - K>([&](auto jc) {
         constexpr int J = K + 1 + decltype(jc)::value;
-        *reinterpret_cast<floatx4*>(lds + W1Lds::PM + (w1_tile(K, J) - (K + 1)) * 256 + 4 * lane) =
+        *reinterpret_cast<floatx4*>(lds + L::PM + (w1_tile<NB>(K, J) - (K + 1)) * 256 + 4 * lane) =
             Pm[decltype(jc)::value];
       });
       // the next pivot block's Schur update first, then its sweep with the rest of
@@ -1284,7 +1292,7 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
       schur(Kc, std::integral_constant<int, 0>{}, Pm);
       pivot_block(std::integral_constant<int, K + 1>{}, [&](auto pc) {
         constexpr int p = decltype(pc)::value;
-        static_for<schur_n(K) - 1>([&](auto vc) {
+        static_for<schur_n<NB>(K) - 1>([&](auto vc) {
           constexpr int u = 1 + decltype(vc)::value;
           if constexpr ((u - 1) % 16 == p) schur(Kc, std::integral_constant<int, u>{}, Pm);
         });
@@ -1300,7 +1308,7 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NT], float (&bcol)[kW1NB],
     static_for<NB - 1 - K>([&](auto jc) {
       constexpr int J = K + 1 + decltype(jc)::value;
       const floatx4 pm = *reinterpret_cast<const floatx4*>(
-          lds + W1Lds::PM + (w1_tile(K, J) - (K + 1)) * 256 + 4 * lane);
+          lds + L::PM + (w1_tile<NB>(K, J) - (K + 1)) * 256 + 4 * lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) pr[r] = fmaf(pm[r], xcol[J], pr[r]);
     });
@@ -1439,6 +1447,14 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 // scal[1] = max |rating| (prep phase).  Explicit: Gram and rhs from the split
 // table Ysp (kp words per row, zero row `zero_row`); implicit: from Y, split in
 // registers after the per-rating confidence weight.
+template <bool ADD_YTY, int NB = kW1NB>
+__device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
+                                                    float scale, float (&bt)[NB], int64_t n_reg,
+                                                    const float* __restrict__ ytyC,
+                                                    unsigned char* smem, int k, float reg,
+                                                    float* __restrict__ xrow, int ld, int row,
+                                                    int32_t* __restrict__ status);
+
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -1497,8 +1513,16 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
   }
   __syncthreads();  // staging area is reused by the solve
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty, X + (int64_t)row * ld,
-                                        ld, row, status);
+  if constexpr (!IMPLICIT && CN == 4) {
+    // rank 33-64 explicit: the W1 block elimination on 4 x 4 tiles (swept diagonal
+    // inverses + fp32 MFMA), in the Gram's scale
+    static_assert(W1LdsT<4>::SIZE <= PanelLds<4>::SIZE, "W1<4> LDS");
+    w1_finish_and_solve<false, 4>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
+                                  X + (int64_t)row * ld, ld, row, status);
+  } else {
+    finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty,
+                                          X + (int64_t)row * ld, ld, row, status);
+  }
 }
 
 __device__ __forceinline__ void block_absmax_publish(float m, unsigned* __restrict__ out) {
@@ -1598,44 +1622,45 @@ __global__ __launch_bounds__(64) void yty_ctab_kernel(const double* __restrict__
 // in that scale: (A + (lambda n / scale) I) x = b / scale  (+ YtY / scale for
 // implicit, from the C-layout table).  Padded dims (k < 128) become identity
 // rows/columns.  bt: per-lane rhs partials (summed over the 4 rating slots here).
-template <bool ADD_YTY>
-__device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[kW1NT], float scale,
-                                                    float (&bt)[kW1NB], int64_t n_reg,
+template <bool ADD_YTY, int NB>
+__device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
+                                                    float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
                                                     int32_t* __restrict__ status) {
+  constexpr int NT_ = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   const float inv = 1.f / scale;  // power of two: exact
-  float bq[kW1NB];
+  float bq[NB];
 #pragma unroll
-  for (int c = 0; c < kW1NB; ++c) {
+  for (int c = 0; c < NB; ++c) {
     const float v = reduce_rows4(bt[c]) * inv;
-    bq[c] = m * kW1NB + c < k ? v : 0.f;
+    bq[c] = m * NB + c < k ? v : 0.f;
   }
   const float lam = (float)((double)reg * (double)n_reg) * inv;
   if constexpr (ADD_YTY) {
-    static_for<kW1NT>([&](auto tc) {
+    static_for<NT_>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
 #pragma unroll
       for (int r = 0; r < 4; ++r) A[t][r] = fmaf(ytyC[(t * 4 + r) * 64 + lane], inv, A[t][r]);
     });
   }
-  if (k == kW1NB * 16) {  // uniform: no padded dims, lambda on the diagonal only
-    static_for<kW1NB>([&](auto cc) {
+  if (k == NB * 16) {  // uniform: no padded dims, lambda on the diagonal only
+    static_for<NB>([&](auto cc) {
       constexpr int c = decltype(cc)::value;
-      constexpr int t = w1_tile(c, c);
+      constexpr int t = w1_tile<NB>(c, c);
 #pragma unroll
       for (int r = 0; r < 4; ++r) A[t][r] += (4 * q + r == m) ? lam : 0.f;
     });
   } else {
-    static_for<kW1NT>([&](auto tc) {
+    static_for<NT_>([&](auto tc) {
       constexpr int t = decltype(tc)::value;
-      constexpr int c1 = FullTiles<8>::l1(t), c2 = FullTiles<8>::l2(t);
+      constexpr int c1 = FullTiles<NB>::l1(t), c2 = FullTiles<NB>::l2(t);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int i, j;
-        tile_ij<8>(c1, c2, r, i, j);
+        tile_ij<NB>(c1, c2, r, i, j);
         const bool pad = (i >= k) | (j >= k);
         float v = pad ? 0.f : A[t][r];
         if constexpr (c1 == c2) v = (i == j) ? (pad ? 1.f : v + lam) : v;
@@ -1643,7 +1668,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[kW1NT], float s
       }
     });
   }
-  const bool ok = w1_solve<kW1NT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  const bool ok = w1_solve<NB>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 

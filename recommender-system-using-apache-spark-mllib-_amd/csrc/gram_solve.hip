@@ -1568,6 +1568,29 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
 }
 
 // Launch 2: heavy rows — sum their chunk slots in a fixed order (fp64), then solve.
+// Launch 2a (k <= 64): a heavy row's fp64 chunk slots summed element-wise (one
+// thread per slot element, four interleaved partial sums in a fixed order) into its
+// first slot; each thread reads and writes only its own element.
+template <int SLOT>
+__global__ __launch_bounds__(256) void heavy_sum_f64_kernel(const int32_t* __restrict__ slot_begin,
+                                                            double* __restrict__ slots) {
+  const int h = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= SLOT) return;
+  const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
+  if (s1 - s0 <= 1) return;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int s = s0;
+  for (; s + 4 <= s1; s += 4) {
+    a0 += slots[(int64_t)s * SLOT + e];
+    a1 += slots[(int64_t)(s + 1) * SLOT + e];
+    a2 += slots[(int64_t)(s + 2) * SLOT + e];
+    a3 += slots[(int64_t)(s + 3) * SLOT + e];
+  }
+  for (; s < s1; ++s) a0 += slots[(int64_t)s * SLOT + e];
+  slots[(int64_t)s0 * SLOT + e] = (a0 + a1) + (a2 + a3);
+}
+
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
@@ -1581,8 +1604,8 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   double a64[NT][4], b64[CN];
   zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
-  for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
-    add_slot<NT, CN>(slots + (int64_t)s * Cfg<CN>::SLOT, a64, b64, npos);
+  // the row's chunk slots were summed into its first slot (heavy_sum_f64_kernel)
+  add_slot<NT, CN>(slots + (int64_t)slot_begin[h] * Cfg<CN>::SLOT, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
   finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
                                          X + (int64_t)row * ld, ld, row, status);
@@ -2345,10 +2368,14 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                     Y_src, X_dst, ld, k, reg, alpha, yty_packed,  \
                                                     slots, status_dev, scal, Ysp, kp, zero_row);  \
     ALS_LAUNCH_CHECK();                                                                           \
-    if (g2)                                                                                       \
+    if (g2) {                                                                                     \
+      heavy_sum_f64_kernel<Cfg<CN>::SLOT>                                                         \
+          <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots);       \
+      ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
                                                       slots, X_dst, ld, k, reg, yty_packed,       \
                                                       status_dev);                                \
+    }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
   } while (0)
 #define ALS_SOLVE_WG_LAUNCH(IMP)                                                                  \

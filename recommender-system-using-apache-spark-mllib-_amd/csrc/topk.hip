@@ -231,16 +231,24 @@ __device__ __forceinline__ float tk_log2_ref(const float* __restrict__ scal, int
   return __log2f(fmaxf(scal[1], 1e-30f)) + 0.5f * __log2f((float)k);
 }
 
+// Bucket counts: per-workgroup histogram in LDS (rows of similar norm share a
+// bucket, so global atomics per row would serialise), flushed once per nonzero bin.
 __global__ __launch_bounds__(256) void tk_bucket_hist_kernel(const float* __restrict__ V,
                                                              int64_t n_v, int ld, int k,
                                                              const float* __restrict__ scal,
                                                              int32_t* __restrict__ hist) {
+  __shared__ int lh[kTkBuckets];
+  for (int b = threadIdx.x; b < kTkBuckets; b += 256) lh[b] = 0;
+  __syncthreads();
   const float ref = tk_log2_ref(scal, k);
   for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; r < n_v;
        r += ((int64_t)gridDim.x * 256) >> 4) {
     const int b = tk_row_bucket(V, r, ld, k, ref);
-    if ((threadIdx.x & 15) == 0) atomicAdd(hist + b, 1);
+    if ((threadIdx.x & 15) == 0) atomicAdd(lh + b, 1);
   }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kTkBuckets; b += 256)
+    if (lh[b]) atomicAdd(hist + b, lh[b]);
 }
 
 // Exclusive scan of the bucket counts (one workgroup) -> scatter cursors.
@@ -269,16 +277,31 @@ __global__ __launch_bounds__(1024) void tk_bucket_scan_kernel(int32_t* __restric
   }
 }
 
+// Scatter with the same grid as the count pass: a workgroup recounts its rows in
+// LDS, reserves one range per nonzero bin with one global atomic, then places its
+// rows inside those ranges with LDS atomics.
 __global__ __launch_bounds__(256) void tk_bucket_scatter_kernel(const float* __restrict__ V,
                                                                 int64_t n_v, int ld, int k,
                                                                 const float* __restrict__ scal,
                                                                 int32_t* __restrict__ cursor,
                                                                 int32_t* __restrict__ perm) {
+  __shared__ int lh[kTkBuckets];
+  for (int b = threadIdx.x; b < kTkBuckets; b += 256) lh[b] = 0;
+  __syncthreads();
   const float ref = tk_log2_ref(scal, k);
-  for (int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; r < n_v;
-       r += ((int64_t)gridDim.x * 256) >> 4) {
+  const int64_t r0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4;
+  const int64_t rs = ((int64_t)gridDim.x * 256) >> 4;
+  for (int64_t r = r0; r < n_v; r += rs) {
     const int b = tk_row_bucket(V, r, ld, k, ref);
-    if ((threadIdx.x & 15) == 0) perm[atomicAdd(cursor + b, 1)] = (int32_t)r;
+    if ((threadIdx.x & 15) == 0) atomicAdd(lh + b, 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < kTkBuckets; b += 256)
+    if (lh[b]) lh[b] = atomicAdd(cursor + b, lh[b]);  // base of this workgroup's range
+  __syncthreads();
+  for (int64_t r = r0; r < n_v; r += rs) {
+    const int b = tk_row_bucket(V, r, ld, k, ref);
+    if ((threadIdx.x & 15) == 0) perm[atomicAdd(lh + b, 1)] = (int32_t)r;
   }
 }
 
@@ -695,7 +718,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     ALS_LAUNCH_CHECK();
     // sweep order: V rows by decreasing norm (bucketed)
     ALS_HIP(hipMemsetAsync(hist, 0, sizeof(int32_t) * kTkBuckets, st));
-    const int gb = (int)std::min<int64_t>(4096, (n_v * 16 + 255) / 256);
+    const int gb = (int)std::min<int64_t>(512, (n_v * 16 + 255) / 256);
     tk_bucket_hist_kernel<<<gb, 256, 0, st>>>(V, n_v, ld, k, scal, hist);
     ALS_LAUNCH_CHECK();
     tk_bucket_scan_kernel<<<1, 1024, 0, st>>>(hist);

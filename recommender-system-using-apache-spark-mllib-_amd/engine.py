@@ -35,16 +35,26 @@ def ld_for(rank: int) -> int:
 
 
 class Workspace:
-    """One growable device scratch buffer; the library never allocates on a compute call."""
+    """One growable device scratch buffer; the library never allocates on a compute call.
 
-    def __init__(self, device):
+    shared_rating_scale: every block solved with this workspace has the same ratings
+    (ALSCore's user- and item-major CSR of one rating set), so the rating scale word
+    that als_solve_half's phase 8 leaves at the start of the buffer stays valid until
+    another call uses the buffer or it is reallocated; solve_half then skips phase 8."""
+
+    def __init__(self, device, shared_rating_scale: bool = False):
         self.device = device
         self.buf: Optional[torch.Tensor] = None
+        self.shared_rating_scale = shared_rating_scale
+        self.rating_scale_key = None
 
-    def get(self, nbytes: int) -> torch.Tensor:
+    def get(self, nbytes: int, keep_scale: bool = False) -> torch.Tensor:
         nbytes = max(int(nbytes), 256)
         if self.buf is None or self.buf.numel() < nbytes:
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self.rating_scale_key = None
+        if not keep_scale:
+            self.rating_scale_key = None
         return self.buf
 
 
@@ -207,7 +217,13 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
     1 = launch 1, 2 = launch 2; 15 = all in order.  ws_chunks: size the workspace for
     this many heavy-row chunks (>= block.n_chunks; blocks sharing one Y prep)."""
     L = _lib.lib()
-    w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0]))
+    w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0]),
+               keep_scale=True)
+    key = (w.data_ptr(), w.numel())
+    if (phases & 8) and ws.shared_rating_scale and ws.rating_scale_key == key:
+        phases &= ~8  # the rating scale word of this rating set is already in place
+        if phases == 0:
+            return
     check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
                            ptr(block.light_rows), block.n_light, ptr(block.heavy_rows),
                            ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),
@@ -216,6 +232,8 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
                            int(bool(implicit)),
                            float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(), int(phases),
                            stream_ptr(X.device)), "als_solve_half")
+    if (phases & 8) and ws.shared_rating_scale:
+        ws.rating_scale_key = key
 
 
 # ---------------------------------------------------------------------------
@@ -279,7 +297,8 @@ class ALSCore:
         _lib.require_gpu()
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
-        self.ws = Workspace(self.device)
+        # both CSR sides hold the same ratings: one rating scale for every half-sweep
+        self.ws = Workspace(self.device, shared_rating_scale=True)
         u = _to_device(users, torch.int32, self.device)
         i = _to_device(items, torch.int32, self.device)
         r = _to_device(ratings, torch.float32, self.device)

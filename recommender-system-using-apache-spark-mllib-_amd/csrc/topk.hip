@@ -356,23 +356,36 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // tiles cost occupancy (measured: 128 / NK and 192 / NK slower on ML-25M shapes).
 __host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
 
-// Insert candidate (sc, id) into a list sorted by ascending goodness (k-th best at
-// [0]; entries past `top` are sentinels (+inf, -1) that nothing beats; unfilled
-// entries are (-inf, INT_MAX)).  c_j = candidate beats entry j is monotone (true
-// for j < p); the list becomes [.. entries 1..p-1, candidate, entries p..]:
-// independent selects, no chain.  The caller has checked that it beats [0].
+// Register lists hold (score, index) as one 64-bit key whose unsigned order is the
+// ranking order: high word = the score's bits made monotone (sign flip), low word =
+// ~index (a lower index ranks higher on equal scores).  NaN scores are never keys.
+__device__ __forceinline__ uint64_t tk_key(float sc, int id) {
+  const uint32_t u = __float_as_uint(sc + 0.f);  // -0 -> +0: equal scores, equal bits
+  const uint32_t o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((uint64_t)o << 32) | (uint32_t)(~id);
+}
+__device__ __forceinline__ float tk_key_score(uint64_t key) {
+  const uint32_t o = (uint32_t)(key >> 32);
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ int tk_key_index(uint64_t key) { return (int)~(uint32_t)key; }
+constexpr uint64_t kTkKeyOpen = 0;              // unfilled entry: any candidate ranks above it
+constexpr uint64_t kTkKeySentinel = ~0ull;      // entries past `top`: nothing ranks above it
+
+// Insert key `c` into a list sorted ascending (the k-th best at [0]; sentinels past
+// `top`).  c_j = c > key_j is monotone (true for j < p); the list becomes
+// [.. keys 1..p-1, c, keys p..]: independent selects, no chain.  The caller has
+// checked c > [0].
 template <int TOPR>
-__device__ __forceinline__ void tk_insert(float (&sv)[TOPR], int (&iv)[TOPR], float sc, int id) {
-  bool c[TOPR + 1];
+__device__ __forceinline__ void tk_insert(uint64_t (&kv)[TOPR], uint64_t c) {
+  bool gt[TOPR + 1];
 #pragma unroll
-  for (int j = 0; j < TOPR; ++j) c[j] = beats(sc, id, sv[j], iv[j]);
-  c[TOPR] = false;
+  for (int j = 0; j < TOPR; ++j) gt[j] = c > kv[j];
+  gt[TOPR] = false;
 #pragma unroll
   for (int j = 0; j < TOPR; ++j) {
-    const float sn = j + 1 < TOPR ? sv[j + 1] : 0.f;
-    const int in = j + 1 < TOPR ? iv[j + 1] : 0;
-    sv[j] = c[j + 1] ? sn : (c[j] ? sc : sv[j]);
-    iv[j] = c[j + 1] ? in : (c[j] ? id : iv[j]);
+    const uint64_t nx = j + 1 < TOPR ? kv[j + 1] : 0ull;
+    kv[j] = gt[j + 1] ? nx : (gt[j] ? c : kv[j]);
   }
 }
 
@@ -452,13 +465,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
   // TOPR > 0: this lane's row list (owner lanes lane < 16 RG)
   constexpr int NR = TOPR > 0 ? TOPR : 1;
-  float lsv[NR];
-  int liv[NR];
+  uint64_t kv[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    lsv[j] = j < top ? -__builtin_inff() : __builtin_inff();
-    liv[j] = j < top ? 0x7fffffff : -1;
-  }
+  for (int j = 0; j < NR; ++j) kv[j] = j < top ? kTkKeyOpen : kTkKeySentinel;
 
   uint4 pre[PER];
   int pre_p = 0x7fffffff;
@@ -467,7 +476,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     for (int e = 0; e < PER; ++e) {
       const int x = threadIdx.x + 256 * e;
       const int64_t vrow = vb + x / RW;
-      pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW] : make_uint4(0u, 0u, 0u, 0u);
+      // rows past n_v: f16 NaNs, so their scores are NaN and never pass a filter
+      pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW]
+                          : make_uint4(0x7E007E00u, 0x7E007E00u, 0x7E007E00u, 0x7E007E00u);
     }
     if (threadIdx.x < VT) pre_p = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
   };
@@ -505,21 +516,25 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       for (int g = 0; g < RG; ++g) sink += fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
       return;
     }
-    const bool vin = ibase + m < n_v;
     if constexpr (TOPR > 0) {
       // score >= the row's k-th score (a tie may still win on the index: the
       // owner lanes decide with beats()); until the lists are full every block
-      // goes to the owners
+      // goes to the owners.  Rows past n_v score NaN: no test passes them and
+      // beats() rejects them.
+      const bool fullw = __builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0;
+      if (fullw) {
+        bool c = false;
+#pragma unroll
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= (MODE == 2 ? 3.0e38f : ts[g][r]);
+        if (__ballot(c) == 0) return;
+      }
       bool pr[RG][4];
-      bool anyl = false;
 #pragma unroll
       for (int g = 0; g < RG; ++g)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pr[g][r] = vin && (!full || acc[g][r] >= (MODE == 2 ? 3.0e38f : ts[g][r]));
-          anyl = anyl || pr[g][r];
-        }
-      if (__ballot(anyl) == 0) return;
+        for (int r = 0; r < 4; ++r) pr[g][r] = !fullw || acc[g][r] >= ts[g][r];
       if constexpr (MODE == 3) ++n_offer;
       float* st = sblk + w * RG * 256;              // [g][item m][row]
       float* thr = sblk + 4 * RG * 256 + w * RG * 16;  // [g][row] new k-th scores
@@ -542,10 +557,10 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           const int mm = __builtin_ctz(msk);
           msk &= msk - 1;
           const float sc = sg[16 * mm];
-          const int id = bperm[mm];
-          if (beats(sc, id, lsv[0], liv[0])) tk_insert<NR>(lsv, liv, sc, id);
+          const uint64_t c = tk_key(sc, bperm[mm]);
+          if (sc == sc && c > kv[0]) tk_insert<NR>(kv, c);
         }
-        thr[lane] = lsv[0];
+        thr[lane] = kv[0] == kTkKeyOpen ? -__builtin_inff() : tk_key_score(kv[0]);
       }
       asm volatile("" ::: "memory");
 #pragma unroll
@@ -557,11 +572,12 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
       if (!full) {
         const bool open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
-                               liv[0] == 0x7fffffff;
+                               kv[0] == kTkKeyOpen;
         full = __ballot(open_list) == 0;
       }
       return;
     }
+    const bool vin = ibase + m < n_v;
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
       bool hit = !full;
@@ -625,9 +641,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
               idx_out[row * top + e] = e < n_v ? e : -1;
               score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
             } else {
-              const bool real = liv[j] != 0x7fffffff;
-              idx_out[row * top + e] = real ? liv[j] : -1;
-              score_out[row * top + e] = real ? lsv[j] * unscale : -__builtin_inff();
+              const bool real = kv[j] != kTkKeyOpen;
+              idx_out[row * top + e] = real ? tk_key_index(kv[j]) : -1;
+              score_out[row * top + e] = real ? tk_key_score(kv[j]) * unscale : -__builtin_inff();
             }
           }
         }

@@ -659,7 +659,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
 
 static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
 
-constexpr int kTopR = 16;  // register-resident lists for top <= kTopR
+constexpr int kTopR = 16;  // register-resident lists for top <= kTopR (sized 8 / 12 / 16)
 
 static size_t topk_split_lds_bytes(int kq, int rg, int top) {
   const int nk = kq / 32;
@@ -759,7 +759,11 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   } while (0)
 #define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                 \
   do {                                                \
-    if (top <= kTopR)                                 \
+    if (top <= 8)                                     \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 8);              \
+    else if (top <= 12)                               \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 12);             \
+    else if (top <= kTopR)                            \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
     else                                              \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \

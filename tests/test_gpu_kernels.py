@@ -313,7 +313,7 @@ def test_compute_error_kat_on_gpu():
 
 
 # ---------------------------------------------------------------- K5
-@pytest.mark.parametrize("rank,top", [(4, 1), (10, 10), (32, 20), (64, 10), (64, 16), (16, 17), (64, 100),
+@pytest.mark.parametrize("rank,top", [(4, 1), (10, 10), (32, 20), (64, 8), (64, 9), (64, 10), (64, 12), (64, 13), (64, 16), (16, 17), (64, 100),
                                       (64, 256), (96, 10), (128, 100), (128, 253)])
 def test_topk_parity(rank, top):
     rng = np.random.default_rng(rank * 1000 + top)

@@ -25,7 +25,7 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
       reinterpret_cast<const int32_t*>(static_cast<char*>(ws) + 256 + tk_table_bytes(n_v, k));
 #define L(NK, RG, M)                                                                          \
   do {                                                                                        \
-    if (top <= kTopR) {                                                                       \
+    if (top <= kTopR) { /* the product picks 8 / 12 / 16 by top: the dev modes use 16 */    \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, kTopR, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
       topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,  \

@@ -18,7 +18,8 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libals_hip.so")
+# ALS_HIP_LIB: an alternative build of the same ABI (dev A/B runs)
+LIB_PATH = os.environ.get("ALS_HIP_LIB") or os.path.join(_HERE, "libals_hip.so")
 _lib = None
 _lock = threading.Lock()
 

@@ -1210,8 +1210,85 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
   return I + u;
 }
 
-// NB = 8 (rank 65-128, W1 kernels) or 4 (rank 33-64, explicit gram_solve_kernel).
+// Schur complement and Pm products of the W1 elimination.  Both operands of
+// C += X^T Y are 16 x 16 tiles in the C layout, so each product is a handful of
+// MFMAs with no data movement: on v_mfma_f32_16x16x32_f16 lane (q, m) supplies
+// k = 8q..8q+7, i.e. its four C-layout values twice (hi and lo halves).
+// Split f16 (default): the operands are scaled by powers of two and split into
+// f16 hi + lo; [Xh|Xl]^T [Yh|Yh] + [Xh|Xl]^T [Yl|Yl] = (Xh + Xl)^T (Yh + Yl) is
+// two MFMAs (32 cycles; the fp32 form, four v_mfma_f32_16x16x4_f32, takes 128).
+// For the Schur update the two scales cancel (X 2^a, Pm 2^-a, a balancing the
+// two maxima), so the MFMAs accumulate straight into the fp32 tile: no VALU
+// touches the 36 system tiles during the elimination.  The system is first
+// scaled by a power of two (largest diagonal entry -> [2^13, 2^14)), which bounds
+// every Schur complement entry and keeps the scaled operands inside the f16
+// range; pieces are exact to ~2^-22 relative, and entries far below their tile's
+// maximum lose precision only below the fp32 rounding floor of the elimination.
+// (ALS_W1_SCHUR=0 builds the fp32 MFMA form for comparison.)
+#ifndef ALS_W1_SCHUR
+#define ALS_W1_SCHUR 1
+#endif
+// Where it is used (measured, ML-25M shape): the implicit rank-128 light-row
+// kernel (configs[2] 11.0 -> 9.4 ms/iter) and the heavy-row solve.  Not for
+// NB = 4 (rank 33-64: 10 Schur tiles per system, too few to pay for the scaling
+// and splitting) and not in the explicit rank-128 light-row kernel, whose
+// pre-split Gram leaves no registers for the split operands (it spills; 7.8 ->
+// 8.1 ms/iter measured).
 template <int NB>
+constexpr bool kW1SplitSchur = ALS_W1_SCHUR != 0 && NB == 8;
+
+// fp32 form: acc += X^T Y (the MFMA's k index is permuted to 4q + s4).
+__device__ __forceinline__ floatx4 tile_xty(const floatx4& X, const floatx4& Y, floatx4 acc) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(X[s4], Y[s4], acc, 0, 0, 0);
+  return acc;
+}
+
+// Largest value over the wave (every lane gets it; v >= 0, NaN ignored).
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp_f<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp_f<0x141>(v));  // row_half_mirror
+  v = fmaxf(v, dpp_f<0x140>(v));  // row_mirror
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  float c = fmaxf(a, b), d = c;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
+  return fmaxf(c, d);
+}
+
+__device__ __forceinline__ float absmax4(const floatx4& x) {
+  return fmaxf(fmaxf(__builtin_fabsf(x[0]), __builtin_fabsf(x[1])),
+               fmaxf(__builtin_fabsf(x[2]), __builtin_fabsf(x[3])));
+}
+
+// [hi | lo] f16 halves of s * x (s a power of two): hi = f16(s x) and
+// lo = f16(s x - hi), each one v_fma_mix (the fp32 fma inside is exact).
+__device__ __forceinline__ half8v split_hl(const floatx4& x, float s) {
+  uint32_t h01, h23, l01, l23;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=v"(h01) : "v"(x[0]), "v"(s));
+  asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(h01) : "v"(x[1]), "v"(s));
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=v"(h23) : "v"(x[2]), "v"(s));
+  asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(h23) : "v"(x[3]), "v"(s));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
+      : "=v"(l01) : "v"(x[0]), "v"(s), "v"(h01));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(l01) : "v"(x[1]), "v"(s), "v"(h01));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
+      : "=v"(l23) : "v"(x[2]), "v"(s), "v"(h23));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(l23) : "v"(x[3]), "v"(s), "v"(h23));
+  return __builtin_bit_cast(half8v, make_uint4(h01, h23, l01, l23));
+}
+__device__ __forceinline__ half8v dup_hi(const half8v& v) {
+  return __builtin_shufflevector(v, v, 0, 1, 2, 3, 0, 1, 2, 3);
+}
+__device__ __forceinline__ half8v dup_lo(const half8v& v) {
+  return __builtin_shufflevector(v, v, 4, 5, 6, 7, 4, 5, 6, 7);
+}
+
+// NB = 8 (rank 65-128, W1 kernels) or 4 (rank 33-64, explicit gram_solve_kernel).
+template <int NB, bool SPLIT = kW1SplitSchur<NB>>
 __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
                                          float* __restrict__ lds, int k,
                                          float* __restrict__ xrow, int ld) {
@@ -1222,6 +1299,27 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
   float* vec = lds + L::VEC;
   float zcol[NB];
   float dmin = 3.0e38f;
+  if constexpr (SPLIT) {
+    // scale the system by 2^g: largest diagonal entry (= largest entry) -> [2^13, 2^14)
+    float dm = 0.f;
+    static_for<NB>([&](auto cc) { dm = fmaxf(dm, absmax4(A[w1_tile<NB>(cc, cc)])); });
+    const float sg = ldexpf(1.f, split_exponent(wave_max(dm)) - 1);
+#pragma unroll
+    for (int t = 0; t < NB * (NB + 1) / 2; ++t) A[t] *= sg;
+#pragma unroll
+    for (int c = 0; c < NB; ++c) bcol[c] *= sg;
+    if (k < NB * 16) {
+      // padded dims' identity rows -> 2^13 I: a unit pivot far below the scaled
+      // system would put -1/pivot at the top of Gm's range and flush its real
+      // entries out of the split (x_pad stays 0: b_pad = 0, no coupling)
+      static_for<NB>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * q + r == m && m * NB + c >= k) A[w1_tile<NB>(c, c)][r] = 8192.f;
+      });
+    }
+  }
   // bcol[J] for J > 0 holds per-row-group partial sums (summed over the groups when
   // block J becomes the pivot block): start with the full b_J in row group 0
 #pragma unroll
@@ -1254,15 +1352,19 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
     bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);           // row layout
     wave_lds_order();
   };
+  // step-K operands of the split form: block row K ([hi|lo] of sK A_KJ), Pm halves
+  half8v XK[NB], Ph[NB], Pl[NB];
   auto schur = [&](auto Kc, auto uc, const floatx4 (&Pm)[NB]) {
     constexpr int K = decltype(Kc)::value, u = decltype(uc)::value;
     constexpr int I = schur_I<NB>(K, u), J = schur_J<NB>(K, u);
-    floatx4 acc = A[w1_tile<NB>(I, J)];
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(A[w1_tile<NB>(K, I)][s4], Pm[J - K - 1][s4], acc, 0,
-                                                  0, 0);
-    A[w1_tile<NB>(I, J)] = acc;
+    floatx4& C = A[w1_tile<NB>(I, J)];
+    if constexpr (SPLIT) {
+      // C += (2^a X)^T (2^-a Pm): lo halves of Pm first, then the hi halves
+      C = __builtin_amdgcn_mfma_f32_16x16x32_f16(XK[I - K - 1], Pl[J - K - 1], C, 0, 0, 0);
+      C = __builtin_amdgcn_mfma_f32_16x16x32_f16(XK[I - K - 1], Ph[J - K - 1], C, 0, 0, 0);
+    } else {
+      C = tile_xty(A[w1_tile<NB>(K, I)], Pm[J - K - 1], C);
+    }
   };
   pivot_block(std::integral_constant<int, 0>{}, [](auto) {});
   static_for<NB>([&](auto Kc) {
@@ -1272,15 +1374,51 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
     if constexpr (K + 1 < NB) {
       // Pm_J = Gm B_KJ;  b_J += Pm_J^T b_K (per-row-group partials)
       floatx4 Pm[NB];
-      static_for<NB - 1 - K>([&](auto jc) {
-        constexpr int J = K + 1 + decltype(jc)::value;
-        floatx4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(Gm[s4], A[w1_tile<NB>(K, J)][s4], acc, 0, 0, 0);
-        Pm[decltype(jc)::value] = acc;
-        bcol[J] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
-      });
+      if constexpr (SPLIT) {
+        // split block row K and Gm; Pm_J = Gm^T A_KJ on the f16 cores
+        float mx = 0.f;
+        static_for<NB - 1 - K>([&](auto jc) {
+          mx = fmaxf(mx, absmax4(A[w1_tile<NB>(K, K + 1 + decltype(jc)::value)]));
+        });
+        const int eX = split_exponent(wave_max(mx));
+        static_for<NB - 1 - K>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          XK[j] = split_hl(A[w1_tile<NB>(K, K + 1 + j)], ldexpf(1.f, eX));
+        });
+        const int eG = split_exponent(wave_max(absmax4(Gm)));
+        const half8v g = split_hl(Gm, ldexpf(1.f, eG));
+        const half8v gh = dup_hi(g), gl = dup_lo(g);
+        const float invGX = ldexpf(1.f, -eG - eX);
+        float mp = 0.f;
+        static_for<NB - 1 - K>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          // Gm^T X = [Gl|Gl]^T [Xh|Xl] + [Gh|Gh]^T [Xh|Xl]
+          floatx4 acc =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, XK[j], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, XK[j], acc, 0, 0, 0) * invGX;
+          Pm[j] = acc;
+          bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
+          mp = fmaxf(mp, absmax4(acc));
+        });
+        // Schur operands 2^a X and 2^-a Pm: a balances the two maxima (both at
+        // 2^((x + p) / 2)), clamped so neither exceeds 2^15
+        const int eP = split_exponent(wave_max(mp));
+        const int a = min(max((eX - eP) >> 1, -eP), eX);
+        static_for<NB - 1 - K>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          XK[j] = split_hl(A[w1_tile<NB>(K, K + 1 + j)], ldexpf(1.f, a));
+          const half8v p = split_hl(Pm[j], ldexpf(1.f, -a));
+          Ph[j] = dup_hi(p);
+          Pl[j] = dup_lo(p);
+        });
+      } else {
+        static_for<NB - 1 - K>([&](auto jc) {
+          constexpr int J = K + 1 + decltype(jc)::value;
+          const floatx4 acc = tile_xty(Gm, A[w1_tile<NB>(K, J)], floatx4{0.f, 0.f, 0.f, 0.f});
+          Pm[decltype(jc)::value] = acc;
+          bcol[J] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
+        });
+      }
       // Pm of block row K -> LDS for the back substitution (lane-private slots)
       static_for<NB - 1 - K>([&](auto jc) {
         constexpr int J = K + 1 + decltype(jc)::value;
@@ -1447,7 +1585,7 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 // scal[1] = max |rating| (prep phase).  Explicit: Gram and rhs from the split
 // table Ysp (kp words per row, zero row `zero_row`); implicit: from Y, split in
 // registers after the per-rating confidence weight.
-template <bool ADD_YTY, int NB = kW1NB>
+template <bool ADD_YTY, int NB = kW1NB, bool SPLIT = kW1SplitSchur<NB>>
 __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
                                                     float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
@@ -1645,7 +1783,7 @@ __global__ __launch_bounds__(64) void yty_ctab_kernel(const double* __restrict__
 // in that scale: (A + (lambda n / scale) I) x = b / scale  (+ YtY / scale for
 // implicit, from the C-layout table).  Padded dims (k < 128) become identity
 // rows/columns.  bt: per-lane rhs partials (summed over the 4 rating slots here).
-template <bool ADD_YTY, int NB>
+template <bool ADD_YTY, int NB, bool SPLIT>
 __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
                                                     float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
@@ -1691,7 +1829,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
       }
     });
   }
-  const bool ok = w1_solve<NB>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -1758,7 +1896,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  w1_finish_and_solve<IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg, X + (int64_t)row * ld,
+  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT && kW1SplitSchur<kW1NB>>(acc, inv2, bt, n_reg, ytyC, smem, k, reg, X + (int64_t)row * ld,
                                 ld, row, status);
 }
 

@@ -670,9 +670,14 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top) {
 }
 
 // Row groups per workgroup of the split kernel (0: its lists do not fit the LDS).
+// Two groups halve the V traffic per query row, but LDS lists (top > kTopR) of
+// two groups must still leave room for two workgroups per CU: the list inserts
+// are latency-bound and need the second workgroup (measured, configs[4] top-100
+// at rank 128: one 120 KB workgroup per CU 602 ms, two 68 KB ones 480 ms).
 static int topk_split_rg(int k, int top) {
   const int kq = topk_kq(k);
-  if (topk_split_lds_bytes(kq, 2, top) <= (size_t)kLdsBytes) return 2;
+  const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
+  if (topk_split_lds_bytes(kq, 2, top) <= rg2_limit) return 2;
   if (topk_split_lds_bytes(kq, 1, top) <= (size_t)kLdsBytes) return 1;
   return 0;
 }

@@ -350,7 +350,16 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // branch-free bubble pass.  A block with survivors stages its 16 x 16 scores in
 // LDS (one ds_write_b128 per lane); each owner lane takes its row's survivors
 // from the ballots, inserts them, and the new k-th scores go back to the
-// filtering lanes by ds_bpermute.  TOPR = 0 (larger top): sorted lists in LDS,
+// filtering lanes by ds_bpermute.  16 < top <= 128 (TOPR = 32 / 64 / 128, one row
+// group): quad lists — a row's list is split over its four lanes 16j + rho as
+// sorted sub-lists of TOPR / 4 keys; the row's k-th best is the least of their
+// four minima (two lane swaps), an insertion replaces that minimum in the lane
+// holding it, and every row of the wave inserts in the same pass (the LDS path
+// below inserts one candidate per wave at a time: 70 ms vs 13.6 ms of scores at
+// rank 128 top 100 on the ML-25M shape).  The output ranks each entry by counting
+// the larger keys of the four sub-lists.  Used while V has at most 2^18 rows
+// (topk_quad: past that, sparse single insertions dominate and the LDS path is
+// faster).  TOPR = 0 (top > 128, or a larger V): sorted lists in LDS,
 // wave-cooperative insertion (topk_offer).
 // Tile rows: 64 / NK keeps the staging registers at 2 x uint4 per thread; larger
 // tiles cost occupancy (measured: 128 / NK and 192 / NK slower on ML-25M shapes).
@@ -387,6 +396,37 @@ __device__ __forceinline__ void tk_insert(uint64_t (&kv)[TOPR], uint64_t c) {
     const uint64_t nx = j + 1 < TOPR ? kv[j + 1] : 0ull;
     kv[j] = gt[j + 1] ? nx : (gt[j] ? c : kv[j]);
   }
+}
+
+// Quad lists (16 < top <= 128, one row group per workgroup): row rho of a wave is
+// owned by its four lanes 16j + rho, each holding a sorted sub-list of S = TOPR / 4
+// keys (sub-list j has top / 4 (+1 for j < top % 4) live slots, sentinels above).
+// The union is the row's current top set; its k-th best is the smallest [0] of the
+// four, found by two row swaps.  An insertion replaces that minimum in the lane that
+// holds it (tk_insert drops [0]), so the sub-list sizes never change; the rows of a
+// wave insert in parallel, one candidate per row per pass.
+__device__ __forceinline__ uint64_t tk_min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+
+// Value of x in lane (j ^ 1, rho) (X = 16) or (j ^ 2, rho) (X = 32), j = lane / 16.
+template <int X>
+__device__ __forceinline__ uint32_t tk_partner(uint32_t x) {
+  uint32_t a = x, b = x;
+  if constexpr (X == 16)
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  // rows j and j ^ (X / 16) exchanged: a holds the lower row of the pair, b the upper
+  const int j = (threadIdx.x & 63) >> 4;
+  return (j & (X / 16)) ? a : b;
+}
+template <int X>
+__device__ __forceinline__ uint64_t tk_partner64(uint64_t x) {
+  return ((uint64_t)tk_partner<X>((uint32_t)(x >> 32)) << 32) | tk_partner<X>((uint32_t)x);
+}
+// Smallest key over the four lanes of this lane's row.
+__device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
+  x = tk_min_u64(x, tk_partner64<16>(x));
+  return tk_min_u64(x, tk_partner64<32>(x));
 }
 
 // MODE (dev ablation only, tools/dev_topk.hip; the product launches MODE 0):
@@ -463,11 +503,16 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       ti[g][r] = 0x7fffffff;
     }
   bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
-  // TOPR > 0: this lane's row list (owner lanes lane < 16 RG)
-  constexpr int NR = TOPR > 0 ? TOPR : 1;
+  // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
+  // sub-list of row m (every lane: sub-list q)
+  constexpr bool QUAD = TOPR > 16;
+  static_assert(!QUAD || (RG == 1 && TOPR % 4 == 0), "quad lists: one row group");
+  // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
+  constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
+  const int ncap = QUAD ? top / 4 + (q < top % 4 ? 1 : 0) : top;  // live slots of this list
   uint64_t kv[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) kv[j] = j < top ? kTkKeyOpen : kTkKeySentinel;
+  for (int j = 0; j < NR; ++j) kv[j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
 
   uint4 pre[PER];
   int pre_p = 0x7fffffff;
@@ -546,7 +591,28 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
         for (int r = 0; r < 4; ++r) b[g][r] = __ballot(pr[g][r]);
       }
       asm volatile("" ::: "memory");  // LDS is in order within the wave
-      if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
+      if constexpr (QUAD) {
+        // every lane: sub-list q of row m; one candidate per row per pass
+        const int rho = m;
+        uint64_t bb = b[0][0];
+#pragma unroll
+        for (int t = 1; t < 4; ++t) bb = (rho & 3) == t ? b[0][t] : bb;
+        unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
+        const float* sg = st + rho;
+        while (__ballot(msk != 0)) {
+          const bool act = msk != 0;
+          const int mm = act ? __builtin_ctz(msk) : 0;
+          msk &= msk - 1;
+          const float sc = sg[16 * mm];
+          const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
+          const uint64_t gmin = tk_quad_min(kv[0]);
+          // the lowest sub-list whose [0] is the row minimum takes the candidate
+          const uint64_t holders = (__ballot(kv[0] == gmin) >> rho) & 0x0001000100010001ull;
+          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv, c);
+        }
+        const uint64_t gmin = tk_quad_min(kv[0]);
+        if (q == 0) thr[rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
+      } else if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
         const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
         uint64_t bb = b[0][0];
 #pragma unroll
@@ -571,8 +637,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? t4[r] : __builtin_inff();
       }
       if (!full) {
-        const bool open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
-                               kv[0] == kTkKeyOpen;
+        const bool open_list =
+            QUAD ? (((live[0] >> m) & 1u) && kv[0] == kTkKeyOpen)
+                 : (lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) && kv[0] == kTkKeyOpen);
         full = __ballot(open_list) == 0;
       }
       return;
@@ -628,7 +695,68 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     if (lane == 0) score_out[blockIdx.x * 4 + w] = MODE == 1 ? sink : (float)n_offer;
     return;
   }
-  if constexpr (TOPR > 0) {
+  if constexpr (QUAD) {
+    // output position of a real entry = number of real entries above it in the
+    // row's four sub-lists; open slots (fewer than `top` V rows) fill the tail
+    const int64_t row = qbase + 16 * w + m;
+    const bool zero = !((live[0] >> m) & 1u);
+    int rank[NR];
+    int nreal = 0, nopen = 0;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      nreal += (kv[i] != kTkKeyOpen && kv[i] != kTkKeySentinel) ? 1 : 0;
+      nopen += (i < ncap && kv[i] == kTkKeyOpen) ? 1 : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      rank[i] = 0;
+#pragma unroll
+      for (int t = i + 1; t < NR; ++t) rank[i] += kv[t] != kTkKeySentinel ? 1 : 0;
+    }
+    auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
+      constexpr int P = decltype(pc)::value;
+#pragma unroll
+      for (int t = 0; t < NR; ++t) {
+        const uint64_t o = P == 1 ? tk_partner64<16>(kv[t])
+                                  : (P == 2 ? tk_partner64<32>(kv[t])
+                                            : tk_partner64<32>(tk_partner64<16>(kv[t])));
+        if (o != kTkKeySentinel) {
+#pragma unroll
+          for (int i = 0; i < NR; ++i) rank[i] += o > kv[i] ? 1 : 0;
+        }
+      }
+    };
+    count_above(std::integral_constant<int, 1>{});
+    count_above(std::integral_constant<int, 2>{});
+    count_above(std::integral_constant<int, 3>{});
+    const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
+    const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
+    const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
+    const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
+    const int R = nreal + r1 + r2 + r3;
+    const int obase = R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
+    if (row < n_q) {
+      if (zero) {  // every score 0: the first `top` rows, ties by index
+        if (q == 0) {
+          for (int e = 0; e < top; ++e) {
+            idx_out[row * top + e] = e < n_v ? e : -1;
+            score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          if (i < ncap) {
+            const bool real = kv[i] != kTkKeyOpen;
+            const int64_t e = row * top + (real ? rank[i] : obase + i);
+            idx_out[e] = real ? tk_key_index(kv[i]) : -1;
+            score_out[e] = real ? tk_key_score(kv[i]) * unscale : -__builtin_inff();
+          }
+        }
+      }
+    }
+    return;
+  } else if constexpr (TOPR > 0) {
     if (lane < 16 * RG) {
       const int64_t row = qbase + 64 * (lane >> 4) + 16 * w + (lane & 15);
       const bool zero = !((live[lane >> 4] >> (lane & 15)) & 1u);
@@ -659,12 +787,24 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
 
 static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
 
-constexpr int kTopR = 16;  // register-resident lists for top <= kTopR (sized 8 / 12 / 16)
+constexpr int kTopR = 16;   // one owner lane's register list for top <= kTopR (sized 8 / 12 / 16)
+constexpr int kTopQ = 128;  // quad register lists for kTopR < top <= kTopQ (32 / 64 / 100 / 128)
 
-static size_t topk_split_lds_bytes(int kq, int rg, int top) {
+// Quad register lists (kTopR < top <= kTopQ) when V has at most kTopQuadMaxV rows.
+// Measured at rank 128, top 100: 59,047 V rows 70 -> 32 ms (their parallel
+// insertion wins while the lists fill, which is most of the work at this size);
+// 1,000,000 V rows 480 -> 584 ms (past the fill, single sparse insertions dominate
+// and the LDS lists' per-candidate path is cheaper).  The crossover between the two
+// sizes is not measured.
+constexpr int64_t kTopQuadMaxV = int64_t(1) << 18;
+static bool topk_quad(int top, int64_t n_v) {
+  return top > kTopR && top <= kTopQ && n_v <= kTopQuadMaxV;
+}
+
+static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
   const size_t tiles = 16 * 2 * (size_t)tk_vt(nk) * (size_t)(kq / 4 + 2) + 4 * 2 * (size_t)tk_vt(nk);
-  if (top <= kTopR) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
+  if (top <= kTopR || quad) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
   return tiles + (sizeof(float) + sizeof(int)) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
 }
@@ -674,11 +814,12 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top) {
 // two groups must still leave room for two workgroups per CU: the list inserts
 // are latency-bound and need the second workgroup (measured, configs[4] top-100
 // at rank 128: one 120 KB workgroup per CU 602 ms, two 68 KB ones 480 ms).
-static int topk_split_rg(int k, int top) {
+static int topk_split_rg(int k, int top, bool quad) {
   const int kq = topk_kq(k);
+  if (quad) return 1;  // quad lists: one row group
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
-  if (topk_split_lds_bytes(kq, 2, top) <= rg2_limit) return 2;
-  if (topk_split_lds_bytes(kq, 1, top) <= (size_t)kLdsBytes) return 1;
+  if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
+  if (topk_split_lds_bytes(kq, 1, top, false) <= (size_t)kLdsBytes) return 1;
   return 0;
 }
 
@@ -713,7 +854,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   if (n_q == 0) return ALS_OK;
   ALS_REQUIRE(Q && V && idx_out && score_out, ALS_EINVAL, "als_topk: null pointer");
   hipStream_t st = as_stream(stream);
-  const int rg = topk_split_rg(k, top);
+  const bool quad = topk_quad(top, n_v);
+  const int rg = topk_split_rg(k, top, quad);
   ALS_REQUIRE(rg > 0, ALS_EUNSUPPORTED, "als_topk: top %d at rank %d does not fit the LDS", top,
               k);
   ALS_REQUIRE(ws != nullptr && ws_bytes >= als_topk_workspace_bytes(n_q, n_v, k, top),
@@ -751,7 +893,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
         V, n_v, ld, k, kq_shift, scal, perm, vsp);
     ALS_LAUNCH_CHECK();
   }
-  const size_t lds = topk_split_lds_bytes(kq, rg, top);
+  const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
   const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
   const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
 #define ALS_TOPK_SPLIT_LAUNCH2(NK, RG, TR)                                                      \
@@ -770,8 +912,18 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 12);             \
     else if (top <= kTopR)                            \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
-    else                                              \
+    else if (!quad)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
+    else if (RG != 1)                                 \
+      return ALS_EUNSUPPORTED;                        \
+    else if (top <= 32)                               \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 32);              \
+    else if (top <= 64)                               \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 64);              \
+    else if (top <= 100)                              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 100);             \
+    else                                              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, kTopQ);           \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);

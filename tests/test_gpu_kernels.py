@@ -314,7 +314,10 @@ def test_compute_error_kat_on_gpu():
 
 # ---------------------------------------------------------------- K5
 @pytest.mark.parametrize("rank,top", [(4, 1), (10, 10), (32, 20), (64, 8), (64, 9), (64, 10), (64, 12), (64, 13), (64, 16), (16, 17), (64, 100),
-                                      (64, 256), (96, 10), (128, 100), (128, 253)])
+                                      (64, 256), (96, 10), (128, 100), (128, 253),
+                                      # quad register lists (16 < top <= 128) at their size boundaries
+                                      (64, 32), (64, 33), (128, 64), (32, 65), (64, 99), (128, 101), (128, 128),
+                                      (128, 129)])
 def test_topk_parity(rank, top):
     rng = np.random.default_rng(rank * 1000 + top)
     n_q, n_v = 333, 1500
@@ -343,16 +346,17 @@ def test_topk_parity(rank, top):
         assert lst.index(10) < lst.index(20)
 
 
-@pytest.mark.parametrize("rank,n_v", [(64, 20011), (128, 9001), (32, 17), (16, 300)])
-def test_topk_many_tiles_ties_across_tiles(rank, n_v):
+@pytest.mark.parametrize("rank,n_v,top", [(64, 20011, 10), (128, 9001, 10), (32, 17, 10),
+                                          (16, 300, 10), (128, 9001, 100), (64, 20011, 50)])
+def test_topk_many_tiles_ties_across_tiles(rank, n_v, top):
     """Many V tiles, a ragged last tile, and exact ties whose copies sit in different
     tiles and blocks (the lower index must win wherever the copies fall)."""
-    rng = np.random.default_rng(rank + n_v)
-    n_q, top = 261, 10
+    rng = np.random.default_rng(rank + n_v + top)
+    n_q = 261
     Q = rng.standard_normal((n_q, rank)).astype(np.float32)
     Vm = rng.standard_normal((n_v, rank)).astype(np.float32)
     Vm *= (1.0 + 3.0 * (np.arange(n_v) % 97 == 0))[:, None].astype(np.float32)  # strong items
-    pairs = [(a, b) for a, b in ((0, n_v - 1), (5, 4100), (130, 131), (97, 9000)) if b < n_v]
+    pairs = [(a, b) for a, b in ((0, n_v - 1), (5, 4100), (130, 131), (97, 8999)) if b < n_v]
     for a, b in pairs:
         Vm[b] = Vm[a]
     ld = E.ld_for(rank)
@@ -377,7 +381,7 @@ def test_topk_many_tiles_ties_across_tiles(rank, n_v):
     assert any(a in idx[r_] and b in idx[r_] for r_ in range(n_q) for a, b in pairs)
 
 
-@pytest.mark.parametrize("rank,top", [(64, 10), (128, 10), (32, 40)])
+@pytest.mark.parametrize("rank,top", [(64, 10), (128, 10), (32, 40), (128, 100)])
 def test_topk_zero_rows_and_norm_order_ties(rank, top):
     """The sweep visits V by decreasing norm: ties between equal rows far apart in index
     (the large-norm copy visited first) must still resolve to the lower index; all-zero
@@ -389,7 +393,8 @@ def test_topk_zero_rows_and_norm_order_ties(rank, top):
     Vm = (rng.standard_normal((n_v, rank)) * rng.uniform(0.1, 3.0, (n_v, 1))).astype(np.float32)
     Vm[100:140] = 0.0
     big = np.argsort(-np.linalg.norm(Vm, axis=1))[:30]  # strong rows, copied to lower indices
-    for t, b in enumerate(big):
+    low = [t for t in range(100) if t not in set(big.tolist())][:30]  # copies never overwrite a source
+    for t, b in zip(low, big):
         Vm[t] = Vm[b]
     ld = E.ld_for(rank)
     Qd = torch.zeros((n_q, ld), device=DEV)
@@ -407,17 +412,49 @@ def test_topk_zero_rows_and_norm_order_ties(rank, top):
                 assert abs(S[row, idx[row, p_]] - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
         np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
         lst = list(idx[row])
-        for t, b in enumerate(big):  # exact copies: the lower index first
+        for t, b in zip(low, big):  # exact copies: the lower index first
             if t in lst and b in lst:
                 assert lst.index(t) < lst.index(b)
     for row in (0, 7, 299):
         assert list(idx[row]) == list(range(top)) and np.all(sc[row] == 0)
 
 
-def test_topk_fewer_items_than_top():
+@pytest.mark.parametrize("rank,top", [(32, 20), (128, 100)])
+def test_topk_large_v_lds_lists(rank, top):
+    """More than 2^18 V rows: 16 < top <= 128 takes the LDS lists (the configs[4] path)."""
+    rng = np.random.default_rng(rank + top + 7)
+    n_q, n_v = 96, (1 << 18) + 1000
+    Q = rng.standard_normal((n_q, rank)).astype(np.float32)
+    Vm = rng.standard_normal((n_v, rank)).astype(np.float32)
+    Vm[123456] = Vm[7]  # exact tie across the sweep: the lower index first
+    ld = E.ld_for(rank)
+    Qd = torch.zeros((n_q, ld), device=DEV)
+    Qd[:, :rank] = torch.as_tensor(Q).to(DEV)
+    Vd = torch.zeros((n_v, ld), device=DEV)
+    Vd[:, :rank] = torch.as_tensor(Vm).to(DEV)
+    idx, sc = E.topk_rows(Qd, n_q, Vd, n_v, rank, top)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    ref_i, ref_s = O.topk(Q, Vm, top)
+    S = Q.astype(np.float64) @ Vm.astype(np.float64).T
+    for row in range(n_q):
+        if not np.array_equal(idx[row], ref_i[row]):
+            bad = np.nonzero(idx[row] != ref_i[row])[0]
+            for p_ in bad:
+                assert abs(S[row, idx[row, p_]] - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
+        np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
+        lst = list(idx[row])
+        if 7 in lst and 123456 in lst:
+            assert lst.index(7) < lst.index(123456)
+
+
+@pytest.mark.parametrize("n_v,top", [(5, 12), (5, 40), (37, 100), (70, 128)])
+def test_topk_fewer_items_than_top(n_v, top):
+    """Lists that never fill: the real entries in score order, then -1 / -inf."""
     Q = torch.randn(70, 8, device=DEV)
-    Vm = torch.randn(5, 8, device=DEV)
-    idx, sc = E.topk_rows(Q, 70, Vm, 5, 8, 12)
-    idx = idx.cpu().numpy()
-    assert np.all(idx[:, 5:] == -1)
-    assert np.all(np.sort(idx[:, :5], axis=1) == np.arange(5))
+    Vm = torch.randn(n_v, 8, device=DEV)
+    idx, sc = E.topk_rows(Q, 70, Vm, n_v, 8, top)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    assert np.all(idx[:, n_v:] == -1) and np.all(sc[:, n_v:] == -np.inf)
+    assert np.all(np.sort(idx[:, :n_v], axis=1) == np.arange(n_v))
+    ref_i, ref_s = O.topk(Q.cpu().numpy(), Vm.cpu().numpy(), n_v)
+    np.testing.assert_allclose(sc[:, :n_v], ref_s, rtol=1e-5, atol=1e-5)

@@ -15,9 +15,10 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
   if (mode == 0) return als_topk(Q, n_q, V, n_v, ld, k, top, idx, sc, ws, ws_bytes, stream);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int kq = topk_kq(k);
-  const int rg = topk_split_rg(k, top);
+  const bool quad = topk_quad(top, n_v);
+  const int rg = topk_split_rg(k, top, quad);
   if (rg == 0) return -1;
-  const size_t lds = topk_split_lds_bytes(kq, rg, top);
+  const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
   const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
   const float* scal = reinterpret_cast<const float*>(ws);
   const uint4* vsp4 = reinterpret_cast<const uint4*>(static_cast<char*>(ws) + 256);
@@ -30,6 +31,11 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
       topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,  \
                                                                   k, top, scal, idx, dbg);    \
+    } else if (quad) { /* quad lists (rg is 1 here): the dev modes use 128 */                 \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, 1, kTopQ, M>), \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+      topk_split_kernel<NK, 1, kTopQ, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,  \
+                                                                 k, top, scal, idx, dbg);     \
     } else {                                                                                  \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, 0, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \

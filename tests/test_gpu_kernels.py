@@ -204,9 +204,10 @@ def test_full_fit_parity_k128(rank, implicit, alpha):
     report(f"full_fit_per_iteration[rank={rank},implicit={implicit}]", worst)
 
 
-@pytest.mark.parametrize("outlier", [1e2, 1e4, 1e5])
+@pytest.mark.parametrize("outlier,implicit", [(1e2, False), (1e4, False), (1e5, False),
+                                              (1e2, True), (1e4, True)])
 @pytest.mark.parametrize("rank", [16, 64, 128])
-def test_half_sweep_mixed_row_norms(outlier, rank):
+def test_half_sweep_mixed_row_norms(outlier, implicit, rank):
     """The split-f16 scale is one power of two per launch (from max |Y|): a block of
     users whose factors are `outlier` times larger (600 users, own items) must not cost the other rows
     their precision.  The outlier users rate a disjoint set of items, so every
@@ -225,14 +226,15 @@ def test_half_sweep_mixed_row_norms(outlier, rank):
     core.init_factors(rank, seed=3)
     core.U[760:] *= outlier  # dense rows = ids here (ids 0..799 all present)
     U0 = core.U[:, :rank].cpu().numpy()
-    core.half_sweep_items(0.1, False, 1.0)
+    alpha = 40.0 if implicit else 1.0  # implicit: the split-f16 W1 Schur at rank 128
+    core.half_sweep_items(0.1, implicit, alpha)
     torch.cuda.synchronize()
     core.check_status()
     ib = core.item_block
     V_ref = O.half_sweep(ib.row_ptr.cpu().numpy(), ib.col.cpu().numpy(), ib.val.cpu().numpy(),
-                         U0, 0.1, False, 1.0)
+                         U0, 0.1, implicit, alpha)
     ev = rel_row_err(core.V[:, :rank].cpu().numpy(), V_ref)
-    report(f"half_sweep_mixed_norms[x{outlier:g},rank={rank}]", ev)
+    report(f"half_sweep_mixed_norms[x{outlier:g},rank={rank},implicit={implicit}]", ev)
     assert ev <= 1e-4
 
 

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of two builds of the library (ALS_HIP_LIB) on the configs[1]/configs[2]/explicit-k128
 # bench lines, after the full GPU parity suite on the default build.
-# Usage: bash tools/gpu_ab.sh TAG ALT_LIB
+# Usage: bash tools/gpu_ab.sh TAG ALT_LIB  (ALT_LIB: e.g. the fp32-Schur build, csrc sources
+# compiled with -DALS_W1_SCHUR=0 and linked to tools/libals_hip_s0.so)
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-/root/repo}
 TAG=${1:-ab}; ALT=${2:-tools/libals_hip_s0.so}

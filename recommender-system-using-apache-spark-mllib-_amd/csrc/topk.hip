@@ -80,20 +80,39 @@ __global__ __launch_bounds__(256) void tk_absmax_kernel(const float* __restrict_
 constexpr int kTopkMax = 256;
 constexpr int kLdsBytes = 160 * 1024;  // per CU on gfx950 (one workgroup may use it all)
 
+// Lists hold (score, index) as one 64-bit key whose unsigned order is the
+// ranking order: high word = the score's bits made monotone (sign flip), low word =
+// ~index (a lower index ranks higher on equal scores).  NaN scores are never keys.
+__device__ __forceinline__ uint64_t tk_key(float sc, int id) {
+  const uint32_t u = __float_as_uint(sc + 0.f);  // -0 -> +0: equal scores, equal bits
+  const uint32_t o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((uint64_t)o << 32) | (uint32_t)(~id);
+}
+__device__ __forceinline__ float tk_key_score(uint64_t key) {
+  const uint32_t o = (uint32_t)(key >> 32);
+  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+__device__ __forceinline__ int tk_key_index(uint64_t key) { return (int)~(uint32_t)key; }
+constexpr uint64_t kTkKeyOpen = 0;              // unfilled entry: any candidate ranks above it
+constexpr uint64_t kTkKeySentinel = ~0ull;      // entries past `top`: nothing ranks above it
+
 __device__ __forceinline__ bool beats(float s1, int i1, float s2, int i2) {
   return s1 > s2 || (s1 == s2 && i1 < i2);
 }
 
-// Offer one 16 x 16 score block to the sorted per-row lists: acc[r] = score of
-// list row slot0 + 4q + r against V row ibase + m.  Candidates that beat their
-// row's current k-th (score, index) are inserted one at a time by the whole
-// wave (rank by ballot, shift, insert), lowest lane first.
+// Offer one 16 x 16 score block to the sorted per-row lists (64-bit keys, best
+// first): acc[r] = score of list row slot0 + 4q + r against V row ibase + m.
+// Candidates that beat their row's current k-th (score, index) are inserted one at
+// a time by the whole wave (rank by ballot, shift, insert), lowest lane first.  The
+// rank is counted from the tail: past the fill, a new key usually lands in the last
+// 64 entries, so one LDS pass finds it.
 __device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_t n_v,
                                            const int32_t* __restrict__ bperm, float (&ts)[4],
-                                           int (&ti)[4], float* __restrict__ ls,
-                                           int* __restrict__ li, int* __restrict__ len, int slot0,
-                                           int top, unsigned live) {
-  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+                                           int (&ti)[4], uint64_t* __restrict__ lk,
+                                           int* __restrict__ len, int slot0, int top,
+                                           unsigned live) {
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  const int m = lane & 15;
   const bool vin = (int64_t)(ibase + m) < n_v;
   // V row index of table row ibase + m (the sweep is norm-ordered; bperm = the
   // block's slice of the tile's order in LDS)
@@ -111,48 +130,44 @@ __device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_
     const float sc =
         __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mys), L));
     const int itm = __builtin_amdgcn_readlane(vidx, L);
+    const uint64_t ck = tk_key(sc, itm);
     const int slot = slot0 + 4 * (L >> 4) + rL;  // list row within the workgroup
-    float* lsr = ls + slot * top;
-    int* lir = li + slot * top;
+    uint64_t* lkr = lk + slot * top;
     const int n = len[slot];
-    // rank = number of entries that beat the candidate
-    int pos = 0;
-    for (int e0 = 0; e0 < n; e0 += 64) {
-      const int e = e0 + lane;
-      const bool bt = e < n && beats(lsr[e], lir[e], sc, itm);
-      pos += __popcll(__ballot(bt));
+    // pos = number of entries that beat the candidate = n - (entries it beats);
+    // scan 64-entry windows from the tail until one holds an entry that beats it
+    int worse = 0;
+    for (int e1 = n; e1 > 0; e1 -= 64) {
+      const int e = e1 - 64 + lane;
+      const int cnt = __popcll(__ballot(e >= 0 && lkr[e < 0 ? 0 : e] < ck));
+      worse += cnt;
+      if (cnt < (e1 < 64 ? e1 : 64)) break;
     }
+    const int pos = n - worse;
     if (pos < top) {
       const int newn = n + 1 < top ? n + 1 : top;
-      float hs[kTopkMax / 64];
-      int hi[kTopkMax / 64];
+      uint64_t hk[kTopkMax / 64];
 #pragma unroll
       for (int j = 0; j < kTopkMax / 64; ++j) {
         const int e = 64 * j + lane;
-        if (e > pos && e < newn) {
-          hs[j] = lsr[e - 1];
-          hi[j] = lir[e - 1];
-        }
+        if (e > pos && e < newn) hk[j] = lkr[e - 1];
       }
       // reads of the shifted entries land before any lane writes (compiler + HW order)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int j = 0; j < kTopkMax / 64; ++j) {
         const int e = 64 * j + lane;
-        if (e > pos && e < newn) {
-          lsr[e] = hs[j];
-          lir[e] = hi[j];
-        }
+        if (e > pos && e < newn) lkr[e] = hk[j];
       }
       if (lane == 0) {
-        lsr[pos] = sc;
-        lir[pos] = itm;
+        lkr[pos] = ck;
         len[slot] = newn;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (newn == top) {
-        const float ks = lsr[top - 1];
-        const int ki = lir[top - 1];
+        const uint64_t kk = lkr[top - 1];
+        const float ks = tk_key_score(kk);
+        const int ki = tk_key_index(kk);
         if (q == (L >> 4)) {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
@@ -175,7 +190,7 @@ __device__ __forceinline__ void topk_offer(const floatx4& acc, int ibase, int64_
 }
 
 // Write the lists of rows slot0 .. slot0+15 (one wave) to the outputs.
-__device__ __forceinline__ void topk_write(const float* __restrict__ ls, const int* __restrict__ li,
+__device__ __forceinline__ void topk_write(const uint64_t* __restrict__ lk,
                                            const int* __restrict__ len, int slot0, int64_t qbase,
                                            int64_t n_q, int64_t n_v, int top, float unscale,
                                            unsigned live, int32_t* __restrict__ idx_out,
@@ -194,8 +209,9 @@ __device__ __forceinline__ void topk_write(const float* __restrict__ ls, const i
     }
     const int n = len[slot];
     for (int e = lane; e < top; e += 64) {
-      idx_out[row * top + e] = e < n ? li[slot * top + e] : -1;
-      score_out[row * top + e] = e < n ? ls[slot * top + e] * unscale : -__builtin_inff();
+      const uint64_t kk = e < n ? lk[slot * top + e] : 0ull;
+      idx_out[row * top + e] = e < n ? tk_key_index(kk) : -1;
+      score_out[row * top + e] = e < n ? tk_key_score(kk) * unscale : -__builtin_inff();
     }
   }
 }
@@ -365,22 +381,6 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // tiles cost occupancy (measured: 128 / NK and 192 / NK slower on ML-25M shapes).
 __host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
 
-// Register lists hold (score, index) as one 64-bit key whose unsigned order is the
-// ranking order: high word = the score's bits made monotone (sign flip), low word =
-// ~index (a lower index ranks higher on equal scores).  NaN scores are never keys.
-__device__ __forceinline__ uint64_t tk_key(float sc, int id) {
-  const uint32_t u = __float_as_uint(sc + 0.f);  // -0 -> +0: equal scores, equal bits
-  const uint32_t o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-  return ((uint64_t)o << 32) | (uint32_t)(~id);
-}
-__device__ __forceinline__ float tk_key_score(uint64_t key) {
-  const uint32_t o = (uint32_t)(key >> 32);
-  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
-}
-__device__ __forceinline__ int tk_key_index(uint64_t key) { return (int)~(uint32_t)key; }
-constexpr uint64_t kTkKeyOpen = 0;              // unfilled entry: any candidate ranks above it
-constexpr uint64_t kTkKeySentinel = ~0ull;      // entries past `top`: nothing ranks above it
-
 // Insert key `c` into a list sorted ascending (the k-th best at [0]; sentinels past
 // `top`).  c_j = c > key_j is monotone (true for j < p); the list becomes
 // [.. keys 1..p-1, c, keys p..]: independent selects, no chain.  The caller has
@@ -451,12 +451,11 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   extern __shared__ uint4 smem_u4[];
   uint4* tiles = smem_u4;                                     // [2][VT][RS]
   int* tperm = reinterpret_cast<int*>(tiles + 2 * VT * RS);   // [2][VT] V row of each tile row
-  // TOPR == 0: [64 RG rows][top] scores, indices, [64 RG] lengths
+  // TOPR == 0: [64 RG rows][top] keys (best first), [64 RG] lengths
   // TOPR > 0: per wave and group a 16 x 16 score block [item m][row]
-  float* ls = reinterpret_cast<float*>(tperm + 2 * VT);
-  int* li = reinterpret_cast<int*>(ls + 64 * RG * top);
-  int* len = li + 64 * RG * top;
-  float* sblk = ls;
+  uint64_t* lk = reinterpret_cast<uint64_t*>(tperm + 2 * VT);  // 8-byte aligned: VT % 16 == 0
+  int* len = reinterpret_cast<int*>(lk + 64 * RG * top);
+  float* sblk = reinterpret_cast<float*>(lk);
 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   const int64_t qbase = (int64_t)blockIdx.x * 64 * RG;
@@ -655,7 +654,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
       if constexpr (MODE == 3) n_offer += hit ? 1 : 0;
       if (hit)
-        topk_offer(acc[g], (int)ibase, n_v, bperm, ts[g], ti[g], ls, li, len, 64 * g + 16 * w,
+        topk_offer(acc[g], (int)ibase, n_v, bperm, ts[g], ti[g], lk, len, 64 * g + 16 * w,
                    top, live[g]);
     }
     if (!full) {
@@ -781,7 +780,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   }
 #pragma unroll
   for (int g = 0; g < RG; ++g)
-    topk_write(ls, li, len, 64 * g + 16 * w, qbase, n_q, n_v, top, unscale, live[g], idx_out,
+    topk_write(lk, len, 64 * g + 16 * w, qbase, n_q, n_v, top, unscale, live[g], idx_out,
                score_out);
 }
 
@@ -805,7 +804,7 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
   const size_t tiles = 16 * 2 * (size_t)tk_vt(nk) * (size_t)(kq / 4 + 2) + 4 * 2 * (size_t)tk_vt(nk);
   if (top <= kTopR || quad) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
-  return tiles + (sizeof(float) + sizeof(int)) * 64 * (size_t)rg * top +
+  return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
 }
 

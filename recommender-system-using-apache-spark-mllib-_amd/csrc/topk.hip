@@ -373,13 +373,20 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // holding it, and every row of the wave inserts in the same pass (the LDS path
 // below inserts one candidate per wave at a time: 70 ms vs 13.6 ms of scores at
 // rank 128 top 100 on the ML-25M shape).  The output ranks each entry by counting
-// the larger keys of the four sub-lists.  Used while V has at most 2^18 rows
-// (topk_quad: past that, sparse single insertions dominate and the LDS path is
-// faster).  TOPR = 0 (top > 128, or a larger V): sorted lists in LDS,
-// wave-cooperative insertion (topk_offer).
+// the larger keys of the four sub-lists; its tiles are 4x taller (tk_vt_q).
+// TOPR = 0 (top > 128): sorted lists in LDS, wave-cooperative insertion
+// (topk_offer).
 // Tile rows: 64 / NK keeps the staging registers at 2 x uint4 per thread; larger
 // tiles cost occupancy (measured: 128 / NK and 192 / NK slower on ML-25M shapes).
 __host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
+// Quad lists: 4x taller tiles (2x at NK = 1, to keep two workgroups per CU).  The
+// workgroup's barrier per tile couples its waves, so one wave's (rare, long)
+// insertion pass stalls the other three; fewer barriers spread that cost, and the
+// quad kernel is register-bound at two workgroups per CU anyway, which leaves LDS
+// for the taller tiles (measured, configs[4] top-100: 1x 584 ms, 2x 397, 4x 330).
+__host__ __device__ constexpr int tk_vt_q(int nk, bool quad) {
+  return quad ? (nk == 1 ? 2 : 4) * tk_vt(nk) : tk_vt(nk);
+}
 
 // Insert key `c` into a list sorted ascending (the k-th best at [0]; sentinels past
 // `top`).  c_j = c > key_j is monotone (true for j < p); the list becomes
@@ -444,7 +451,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   constexpr int KQ = 32 * NK;
   constexpr int RW = KQ / 4;           // uint4 per split row (KQ hi + KQ lo halves)
   constexpr int RS = RW + 2;           // LDS row stride in uint4 (bank-conflict-free)
-  constexpr int VT = tk_vt(NK);        // V rows per tile
+  constexpr int VT = tk_vt_q(NK, TOPR > 16);  // V rows per tile
   constexpr int NC = VT / 16;          // 16-row score blocks per tile
   constexpr int PER = VT * RW / 256;   // staged uint4 per thread per tile
   static_assert(PER * 256 == VT * RW, "tile staging");
@@ -789,20 +796,17 @@ static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
 constexpr int kTopR = 16;   // one owner lane's register list for top <= kTopR (sized 8 / 12 / 16)
 constexpr int kTopQ = 128;  // quad register lists for kTopR < top <= kTopQ (32 / 64 / 100 / 128)
 
-// Quad register lists (kTopR < top <= kTopQ) when V has at most kTopQuadMaxV rows.
-// Measured at rank 128, top 100: 59,047 V rows 70 -> 32 ms (their parallel
-// insertion wins while the lists fill, which is most of the work at this size);
-// 1,000,000 V rows 480 -> 584 ms (past the fill, single sparse insertions dominate
-// and the LDS lists' per-candidate path is cheaper).  The crossover between the two
-// sizes is not measured.
-constexpr int64_t kTopQuadMaxV = int64_t(1) << 18;
+// Quad register lists for kTopR < top <= kTopQ.  Measured at rank 128, top 100
+// against the LDS lists: 59,047 V rows 70 -> 21 ms, 1,000,000 V rows 456 -> 330 ms.
 static bool topk_quad(int top, int64_t n_v) {
-  return top > kTopR && top <= kTopQ && n_v <= kTopQuadMaxV;
+  (void)n_v;
+  return top > kTopR && top <= kTopQ;
 }
 
 static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
-  const size_t tiles = 16 * 2 * (size_t)tk_vt(nk) * (size_t)(kq / 4 + 2) + 4 * 2 * (size_t)tk_vt(nk);
+  const size_t vt = (size_t)tk_vt_q(nk, quad);
+  const size_t tiles = 16 * 2 * vt * (size_t)(kq / 4 + 2) + 4 * 2 * vt;
   if (top <= kTopR || quad) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
   return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;

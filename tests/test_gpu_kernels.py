@@ -421,9 +421,9 @@ def test_topk_zero_rows_and_norm_order_ties(rank, top):
         assert list(idx[row]) == list(range(top)) and np.all(sc[row] == 0)
 
 
-@pytest.mark.parametrize("rank,top", [(32, 20), (128, 100)])
+@pytest.mark.parametrize("rank,top", [(32, 20), (128, 100), (64, 200)])
 def test_topk_large_v_lds_lists(rank, top):
-    """More than 2^18 V rows: 16 < top <= 128 takes the LDS lists (the configs[4] path)."""
+    """More than 2^18 V rows (many tall quad-list tiles, a ragged last one), as at configs[4]."""
     rng = np.random.default_rng(rank + top + 7)
     n_q, n_v = 96, (1 << 18) + 1000
     Q = rng.standard_normal((n_q, rank)).astype(np.float32)

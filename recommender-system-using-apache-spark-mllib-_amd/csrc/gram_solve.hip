@@ -1236,6 +1236,12 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 // 8.1 ms/iter measured).
 template <int NB>
 constexpr bool kW1SplitSchur = ALS_W1_SCHUR != 0 && NB == 8;
+// ALS_W1_EXPLICIT_SPLIT=1: the explicit light-row kernel takes the split Schur with
+// fp32 Pm products (fewer live split operands: 24 B of spill instead of 56).  Measured
+// neutral (ML-25M rank 128 7.93 -> 7.88 ms/iter, configs[3] 398 -> 401 ms), so off.
+#ifndef ALS_W1_EXPLICIT_SPLIT
+#define ALS_W1_EXPLICIT_SPLIT 0
+#endif
 
 // fp32 form: acc += X^T Y (the MFMA's k index is permuted to 4q + s4).
 __device__ __forceinline__ floatx4 tile_xty(const floatx4& X, const floatx4& Y, floatx4 acc) {
@@ -1288,7 +1294,7 @@ __device__ __forceinline__ half8v dup_lo(const half8v& v) {
 }
 
 // NB = 8 (rank 65-128, W1 kernels) or 4 (rank 33-64, explicit gram_solve_kernel).
-template <int NB, bool SPLIT = kW1SplitSchur<NB>>
+template <int NB, bool SPLIT = kW1SplitSchur<NB>, bool SPLIT_PM = true>
 __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
                                          float* __restrict__ lds, int k,
                                          float* __restrict__ xrow, int ld) {
@@ -1375,31 +1381,42 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
       // Pm_J = Gm B_KJ;  b_J += Pm_J^T b_K (per-row-group partials)
       floatx4 Pm[NB];
       if constexpr (SPLIT) {
-        // split block row K and Gm; Pm_J = Gm^T A_KJ on the f16 cores
+        // block row K's scale; Pm_J = Gm^T A_KJ (split f16 with SPLIT_PM, else fp32)
         float mx = 0.f;
         static_for<NB - 1 - K>([&](auto jc) {
           mx = fmaxf(mx, absmax4(A[w1_tile<NB>(K, K + 1 + decltype(jc)::value)]));
         });
         const int eX = split_exponent(wave_max(mx));
-        static_for<NB - 1 - K>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          XK[j] = split_hl(A[w1_tile<NB>(K, K + 1 + j)], ldexpf(1.f, eX));
-        });
-        const int eG = split_exponent(wave_max(absmax4(Gm)));
-        const half8v g = split_hl(Gm, ldexpf(1.f, eG));
-        const half8v gh = dup_hi(g), gl = dup_lo(g);
-        const float invGX = ldexpf(1.f, -eG - eX);
         float mp = 0.f;
-        static_for<NB - 1 - K>([&](auto jc) {
-          constexpr int j = decltype(jc)::value;
-          // Gm^T X = [Gl|Gl]^T [Xh|Xl] + [Gh|Gh]^T [Xh|Xl]
-          floatx4 acc =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, XK[j], floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, XK[j], acc, 0, 0, 0) * invGX;
-          Pm[j] = acc;
-          bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
-          mp = fmaxf(mp, absmax4(acc));
-        });
+        if constexpr (SPLIT_PM) {
+          static_for<NB - 1 - K>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            XK[j] = split_hl(A[w1_tile<NB>(K, K + 1 + j)], ldexpf(1.f, eX));
+          });
+          const int eG = split_exponent(wave_max(absmax4(Gm)));
+          const half8v g = split_hl(Gm, ldexpf(1.f, eG));
+          const half8v gh = dup_hi(g), gl = dup_lo(g);
+          const float invGX = ldexpf(1.f, -eG - eX);
+          static_for<NB - 1 - K>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            // Gm^T X = [Gl|Gl]^T [Xh|Xl] + [Gh|Gh]^T [Xh|Xl]
+            floatx4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, XK[j],
+                                                                floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, XK[j], acc, 0, 0, 0) * invGX;
+            Pm[j] = acc;
+            bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
+            mp = fmaxf(mp, absmax4(acc));
+          });
+        } else {
+          static_for<NB - 1 - K>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const floatx4 acc =
+                tile_xty(Gm, A[w1_tile<NB>(K, K + 1 + j)], floatx4{0.f, 0.f, 0.f, 0.f});
+            Pm[j] = acc;
+            bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
+            mp = fmaxf(mp, absmax4(acc));
+          });
+        }
         // Schur operands 2^a X and 2^-a Pm: a balances the two maxima (both at
         // 2^((x + p) / 2)), clamped so neither exceeds 2^15
         const int eP = split_exponent(wave_max(mp));
@@ -1585,7 +1602,7 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 // scal[1] = max |rating| (prep phase).  Explicit: Gram and rhs from the split
 // table Ysp (kp words per row, zero row `zero_row`); implicit: from Y, split in
 // registers after the per-rating confidence weight.
-template <bool ADD_YTY, int NB = kW1NB, bool SPLIT = kW1SplitSchur<NB>>
+template <bool ADD_YTY, int NB = kW1NB, bool SPLIT = kW1SplitSchur<NB>, bool SPLIT_PM = true>
 __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
                                                     float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
@@ -1783,7 +1800,7 @@ __global__ __launch_bounds__(64) void yty_ctab_kernel(const double* __restrict__
 // in that scale: (A + (lambda n / scale) I) x = b / scale  (+ YtY / scale for
 // implicit, from the C-layout table).  Padded dims (k < 128) become identity
 // rows/columns.  bt: per-lane rhs partials (summed over the 4 rating slots here).
-template <bool ADD_YTY, int NB, bool SPLIT>
+template <bool ADD_YTY, int NB, bool SPLIT, bool SPLIT_PM>
 __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
                                                     float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
@@ -1829,7 +1846,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
       }
     });
   }
-  const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  const bool ok = w1_solve<NB, SPLIT, SPLIT_PM>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -1896,7 +1913,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT && kW1SplitSchur<kW1NB>>(acc, inv2, bt, n_reg, ytyC, smem, k, reg, X + (int64_t)row * ld,
+  w1_finish_and_solve<IMPLICIT, kW1NB, ALS_W1_EXPLICIT_SPLIT ? kW1SplitSchur<kW1NB> : (IMPLICIT && kW1SplitSchur<kW1NB>), IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg, X + (int64_t)row * ld,
                                 ld, row, status);
 }
 

@@ -182,7 +182,16 @@ def topk_roofline(n_q: int, n_v: int, k: int, ms: float, top: int):
            "issued_f16_mfma_tflops": issued / s / 1e12,
            "mfma_frac": issued / s / 1e12 / PEAK_F16_MFMA_TFLOPS,
            "bound": "mfma", "unit": "TFLOP/s"}
-    pmc = load_pmc(f"topk_split_kernel<{kq // 32},", prefix=True)
+    # the launched variant (csrc/topk.hip als_topk): <NK, row groups, list kind, 0>
+    nk = kq // 32
+    if top <= 16:
+        rg, tr = 2, (8 if top <= 8 else (12 if top <= 12 else 16))
+    elif top <= 128:  # quad register lists, one row group
+        rg, tr = 1, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
+    else:
+        rg, tr = None, 0
+    out["kernel"] = f"topk_split_kernel<{nk},{rg if rg else '?'},{tr},0>"
+    pmc = load_pmc(out["kernel"]) if rg else None
     if pmc:
         out["pmc"] = {k_: pmc.get(k_) for k_ in ("mfma_busy_frac", "valu_busy_frac",
                                                  "pmc_run_avg_ns")}

@@ -103,8 +103,10 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * fp32 sums within a task of <= 2048 ratings, fp64 across a heavy row's tasks;
  * solved by a square-root-free block LDL^T (the solution of Spark's Cholesky
  * dppsv) in fp32, stored fp32 into X_dst[row*ld ..].  k <= 128, n_src < 2^31.
- * Measured against an fp64 restatement: <= 5e-6 relative per row (parity bar
- * 1e-4, tests/test_gpu_kernels.py).  yty_packed (implicit only): lower-packed
+ * Parity bar: 1e-4 relative per row against the fp64 restatement of Spark's
+ * dspr + dppsv (oracle/); the measured maxima per configuration (ranks 1-128,
+ * explicit/implicit, full-size half-sweeps) are in DESIGN.md section 1 and
+ * tests/test_gpu_kernels.py / test_gpu_configs.py.  yty_packed (implicit only): lower-packed
  * fp64 k_pad x k_pad Gram from als_yty.  status_dev: device int32, set to
  * (row+1) of a row whose Cholesky pivot was not positive (0 = all rows ok;
  * Spark raises from dppsv in that case).  ws: 16-byte aligned.
@@ -162,9 +164,10 @@ int als_rmse_partial(const int32_t* u, const int32_t* i, const float* r, int64_t
  * score <q, v>, ordered by score descending then index ascending.
  * idx_out[n_q*top] (dense row index of V, -1 when n_v < top), score_out[n_q*top].
  * Scores: fp32-grade products on the f16 matrix cores (q and v split into f16
- * hi + lo after power-of-two scaling, ~2^-21 relative to |q||v|); fp32 MFMA when
- * the lists need more LDS than the split kernel leaves.  k <= 128, top <= 256
- * (<= 253 at k > 64: LDS).  The n_q x n_v score matrix is never materialised.
+ * hi + lo after power-of-two scaling, ~2^-21 relative to |q||v|) for every k and
+ * top.  Lists: registers of one owner lane for top <= 16, four-lane ("quad")
+ * register lists for top <= 128, sorted LDS lists above.  k <= 128, top <= 256.
+ * The n_q x n_v score matrix is never materialised.
  * Workspace (16-byte aligned): scale words + the split copy of V. */
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top);
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v,

@@ -12,8 +12,7 @@
 //    2048-rating chunk of a heavy row; light rows arrive longest-first (LPT).
 //    k <= 64: one wavefront per task (gram_solve_kernel<CN>); 64 < k <= 128: one
 //    wavefront per task with the whole 128 x 128 system in its registers
-//    (gram_solve_w1_kernel, "W1"; gram_solve_wg_kernel = 4-wave alternative,
-//    ALS_K128_PATH=wg).
+//    (gram_solve_w1_kernel, "W1").  One code path per (k range, implicit).
 //  * Gram on the f16 matrix cores with fp32-grade products: every operand t is
 //    carried as hi = f16_rn(t), lo = f16_rn(t - hi) after a power-of-two scale
 //    (largest |t| in [2^14, 2^15), from max |Y| and max |r| computed on the
@@ -33,10 +32,12 @@
 //  * Normal equations as CholeskySolver.solve: A_ii += lambda * n (n = #ratings,
 //    implicit: #ratings > 0), implicit YtY merged in fp64 before the one
 //    rounding to fp32; padded dims get identity rows and zero rhs.
-//  * Solve (fp32, same solution as Spark's dppsv): k <= 64 column-per-lane panel
-//    LDL^T with the trailing tiles on fp32 MFMA; W1 block elimination with
-//    16 x 16 diagonal inverses by the sweep operator (VALU, DPP broadcasts) and
-//    the Pm / Schur products on fp32 MFMA (see w1_solve).
+//  * Solve (fp32, same solution as Spark's dppsv): k <= 32 column-per-lane panel
+//    LDL^T with the trailing tiles on fp32 MFMA; k in (32, 64] and (64, 128]:
+//    block elimination with 16 x 16 diagonal inverses by the sweep operator
+//    (VALU, DPP broadcasts) and the Pm / Schur products on the matrix cores —
+//    split f16 (fp32-grade) for rank 65-128 implicit light rows and heavy rows,
+//    fp32 MFMA for the explicit light rows and rank <= 64 (see w1_solve).
 //  * YtY (K2b): 512-row tasks of the same MFMA Gram, fp64 slots, parallel slot
 //    sum, fixed order.
 #include "als_common.h"
@@ -1224,10 +1225,6 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 // every Schur complement entry and keeps the scaled operands inside the f16
 // range; pieces are exact to ~2^-22 relative, and entries far below their tile's
 // maximum lose precision only below the fp32 rounding floor of the elimination.
-// (ALS_W1_SCHUR=0 builds the fp32 MFMA form for comparison.)
-#ifndef ALS_W1_SCHUR
-#define ALS_W1_SCHUR 1
-#endif
 // Where it is used (measured, ML-25M shape): the implicit rank-128 light-row
 // kernel (configs[2] 11.0 -> 9.4 ms/iter) and the heavy-row solve.  Not for
 // NB = 4 (rank 33-64: 10 Schur tiles per system, too few to pay for the scaling
@@ -1235,13 +1232,7 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 // pre-split Gram leaves no registers for the split operands (it spills; 7.8 ->
 // 8.1 ms/iter measured).
 template <int NB>
-constexpr bool kW1SplitSchur = ALS_W1_SCHUR != 0 && NB == 8;
-// ALS_W1_EXPLICIT_SPLIT=1: the explicit light-row kernel takes the split Schur with
-// fp32 Pm products (fewer live split operands: 24 B of spill instead of 56).  Measured
-// neutral (ML-25M rank 128 7.93 -> 7.88 ms/iter, configs[3] 398 -> 401 ms), so off.
-#ifndef ALS_W1_EXPLICIT_SPLIT
-#define ALS_W1_EXPLICIT_SPLIT 0
-#endif
+constexpr bool kW1SplitSchur = NB == 8;
 
 // fp32 form: acc += X^T Y (the MFMA's k index is permuted to 4q + s4).
 __device__ __forceinline__ floatx4 tile_xty(const floatx4& X, const floatx4& Y, floatx4 acc) {
@@ -1294,7 +1285,7 @@ __device__ __forceinline__ half8v dup_lo(const half8v& v) {
 }
 
 // NB = 8 (rank 65-128, W1 kernels) or 4 (rank 33-64, explicit gram_solve_kernel).
-template <int NB, bool SPLIT = kW1SplitSchur<NB>, bool SPLIT_PM = true>
+template <int NB, bool SPLIT = kW1SplitSchur<NB>>
 __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
                                          float* __restrict__ lds, int k,
                                          float* __restrict__ xrow, int ld) {
@@ -1381,42 +1372,31 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
       // Pm_J = Gm B_KJ;  b_J += Pm_J^T b_K (per-row-group partials)
       floatx4 Pm[NB];
       if constexpr (SPLIT) {
-        // block row K's scale; Pm_J = Gm^T A_KJ (split f16 with SPLIT_PM, else fp32)
+        // block row K's scale; Pm_J = Gm^T A_KJ on split f16
         float mx = 0.f;
         static_for<NB - 1 - K>([&](auto jc) {
           mx = fmaxf(mx, absmax4(A[w1_tile<NB>(K, K + 1 + decltype(jc)::value)]));
         });
         const int eX = split_exponent(wave_max(mx));
         float mp = 0.f;
-        if constexpr (SPLIT_PM) {
-          static_for<NB - 1 - K>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            XK[j] = split_hl(A[w1_tile<NB>(K, K + 1 + j)], ldexpf(1.f, eX));
-          });
-          const int eG = split_exponent(wave_max(absmax4(Gm)));
-          const half8v g = split_hl(Gm, ldexpf(1.f, eG));
-          const half8v gh = dup_hi(g), gl = dup_lo(g);
-          const float invGX = ldexpf(1.f, -eG - eX);
-          static_for<NB - 1 - K>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            // Gm^T X = [Gl|Gl]^T [Xh|Xl] + [Gh|Gh]^T [Xh|Xl]
-            floatx4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, XK[j],
-                                                                floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, XK[j], acc, 0, 0, 0) * invGX;
-            Pm[j] = acc;
-            bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
-            mp = fmaxf(mp, absmax4(acc));
-          });
-        } else {
-          static_for<NB - 1 - K>([&](auto jc) {
-            constexpr int j = decltype(jc)::value;
-            const floatx4 acc =
-                tile_xty(Gm, A[w1_tile<NB>(K, K + 1 + j)], floatx4{0.f, 0.f, 0.f, 0.f});
-            Pm[j] = acc;
-            bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
-            mp = fmaxf(mp, absmax4(acc));
-          });
-        }
+        static_for<NB - 1 - K>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          XK[j] = split_hl(A[w1_tile<NB>(K, K + 1 + j)], ldexpf(1.f, eX));
+        });
+        const int eG = split_exponent(wave_max(absmax4(Gm)));
+        const half8v g = split_hl(Gm, ldexpf(1.f, eG));
+        const half8v gh = dup_hi(g), gl = dup_lo(g);
+        const float invGX = ldexpf(1.f, -eG - eX);
+        static_for<NB - 1 - K>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          // Gm^T X = [Gl|Gl]^T [Xh|Xl] + [Gh|Gh]^T [Xh|Xl]
+          floatx4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, XK[j],
+                                                              floatx4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, XK[j], acc, 0, 0, 0) * invGX;
+          Pm[j] = acc;
+          bcol[K + 1 + j] += acc[0] * bk[0] + acc[1] * bk[1] + acc[2] * bk[2] + acc[3] * bk[3];
+          mp = fmaxf(mp, absmax4(acc));
+        });
         // Schur operands 2^a X and 2^-a Pm: a balances the two maxima (both at
         // 2^((x + p) / 2)), clamped so neither exceeds 2^15
         const int eP = split_exponent(wave_max(mp));
@@ -1602,7 +1582,7 @@ __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 // scal[1] = max |rating| (prep phase).  Explicit: Gram and rhs from the split
 // table Ysp (kp words per row, zero row `zero_row`); implicit: from Y, split in
 // registers after the per-rating confidence weight.
-template <bool ADD_YTY, int NB = kW1NB, bool SPLIT = kW1SplitSchur<NB>, bool SPLIT_PM = true>
+template <bool ADD_YTY, int NB = kW1NB, bool SPLIT = kW1SplitSchur<NB>>
 __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
                                                     float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
@@ -1800,7 +1780,7 @@ __global__ __launch_bounds__(64) void yty_ctab_kernel(const double* __restrict__
 // in that scale: (A + (lambda n / scale) I) x = b / scale  (+ YtY / scale for
 // implicit, from the C-layout table).  Padded dims (k < 128) become identity
 // rows/columns.  bt: per-lane rhs partials (summed over the 4 rating slots here).
-template <bool ADD_YTY, int NB, bool SPLIT, bool SPLIT_PM>
+template <bool ADD_YTY, int NB, bool SPLIT>
 __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) / 2],
                                                     float scale, float (&bt)[NB], int64_t n_reg,
                                                     const float* __restrict__ ytyC,
@@ -1846,7 +1826,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
       }
     });
   }
-  const bool ok = w1_solve<NB, SPLIT, SPLIT_PM>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
 }
 
@@ -1913,8 +1893,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  w1_finish_and_solve<IMPLICIT, kW1NB, ALS_W1_EXPLICIT_SPLIT ? kW1SplitSchur<kW1NB> : (IMPLICIT && kW1SplitSchur<kW1NB>), IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg, X + (int64_t)row * ld,
-                                ld, row, status);
+  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
+                                               X + (int64_t)row * ld, ld, row, status);
 }
 
 // Launch 2 (W1): heavy rows — fp64 sums of the fp32 chunk partials in a fixed
@@ -2010,269 +1990,12 @@ __global__ __launch_bounds__(64) void yty_reduce_kernel(const double* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// k in (64, 128]: one workgroup of 4 wavefronts per system (CN = 8, NB = 8
-// block rows, 36 upper tiles).  Wave R accumulates the tiles of WgTiles<R>
-// (10/10/8/8) with the split f16 Gram and keeps them in registers through the
-// factorisation.  The panel LDL^T of panel_ldl_solve, spread over the waves:
-//   (a) owners write block row K (column-major) to the tile slots  | barrier
-//   (b) wave w: lanes 0..15 the diagonal block (every wave, the same
-//       arithmetic; wave 0 publishes it), lanes 16..63 the off-diagonal tiles
-//       J = K+1+3w .. K+3+3w; U columns and updated rhs back to LDS  | barrier
-//   (c) each wave: MFMA trailing update of its own tiles (I > K)
-// then wave 0 back-substitutes.  The rhs of column j of tile J lives in RB[16J+j]
-// between block rows.
-// LDS (floats): tile slots 36 x 288 | z, d, x, rb 4 x 128 = 43.5 KB: three
-// workgroups (12 waves, 3 per SIMD) per CU.
+// K2b at 64 < k <= 128: one workgroup of 4 wavefronts per YtY task, wave R
+// accumulating the tiles of WgTiles<R> (10/10/8/8 of the 36 upper tiles).
 // ---------------------------------------------------------------------------
 constexpr int kWgNB = 8;
-
-struct WgLds {
-  static constexpr int NB = kWgNB, NT = NB * (NB + 1) / 2, CS = 18;
-  static constexpr int T = 0, Z = NT * 16 * CS, D = Z + 16 * NB, X = D + 16 * NB,
-                       RB = X + 16 * NB, SIZE = RB + 16 * NB;
-};
-
-template <int R>
-__device__ __forceinline__ bool wg_panel_solve(floatx4 (&A)[WgTiles<R>::N], float* __restrict__ lds,
-                                               int k, float* __restrict__ xrow, int ld) {
-  typedef WgTiles<R> TS;
-  typedef WgLds Lo;
-  constexpr int NB = kWgNB, CS = Lo::CS;
-  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  float* Zv = lds + Lo::Z;
-  float* Dv = lds + Lo::D;
-  float* Xv = lds + Lo::X;
-  float* RBv = lds + Lo::RB;
-  auto slot = [&](int I, int J) { return lds + Lo::T + tile_index(NB, I, J) * 16 * CS; };
-  bool okl = true;  // this lane: every pivot of its diagonal lane was > 0
-  static_for<NB>([&](auto Kc) {
-    constexpr int K = decltype(Kc)::value;
-    // (a) owners: block row K -> column-major slots
-    static_for<TS::N>([&](auto tc) {
-      constexpr int t = decltype(tc)::value;
-      if constexpr (TS::g1(t) == K) {
-        const floatx4 v = A[t];
-        float2* dst = reinterpret_cast<float2*>(slot(K, TS::g2(t)) + m * CS + 4 * q);
-        dst[0] = make_float2(v[0], v[1]);
-        dst[1] = make_float2(v[2], v[3]);
-      }
-    });
-    __syncthreads();
-    // (b) panel: lanes 0..15 diagonal block, lanes 16.. tiles K+1+3R ..
-    constexpr int NOFF = NB - 1 - K;  // off-diagonal tiles in block row K
-    // Every active wave factors the diagonal block B_KK redundantly from its slot,
-    // so wave 0 must not overwrite that slot (nor the diagonal rhs RB[16K..]) until
-    // all waves have read it: its U_KK columns stay in R16 until after the barrier.
-    float R16[16];
-    if constexpr (R == 0 || 3 * R < NOFF) {
-      const int Jl0 = q == 0 ? K : K + 3 * R + q;
-      const bool col_ok = Jl0 < NB;
-      const int Jl = col_ok ? Jl0 : K;
-      float* colp = slot(K, Jl) + m * CS;
-#pragma unroll
-      for (int c2 = 0; c2 < 8; ++c2) {
-        const float2 v = *reinterpret_cast<const float2*>(colp + 2 * c2);
-        R16[2 * c2] = v.x; R16[2 * c2 + 1] = v.y;
-      }
-      float rb = RBv[16 * Jl + m];
-      float myd = 1.f;
-      static_for<16>([&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        float a[16];
-        float bp;
-        pivot_broadcast<16>(R16, rb, p, a, bp);
-        const float d = a[p];
-        const float rd = rcp_t(d);
-        const float f = gate_above<p>(R16[p] * rd);
-        rb = fmaf(-f, bp, rb);
-        pivot_update<16>(R16, a, p, f);
-        R16[p] = f;
-        myd = put_lane<p>(myd, d);
-      });
-      okl = okl && (myd > 0.f);  // lanes >= 16 keep myd = 1; NaN pivots fail
-      if (col_ok && q > 0) {
-#pragma unroll
-        for (int c2 = 0; c2 < 8; ++c2)
-          *reinterpret_cast<float2*>(colp + 2 * c2) = make_float2(R16[2 * c2], R16[2 * c2 + 1]);
-        RBv[16 * Jl + m] = rb;
-      }
-      if (R == 0 && lane < 16) {
-        Zv[K * 16 + lane] = rb;
-        Dv[K * 16 + lane] = myd;
-      }
-    }
-    __syncthreads();
-    if constexpr (R == 0) {
-      // U_KK columns -> the diagonal slot, now that no wave reads B_KK any more
-      // (read again only by this wave's back substitution)
-      if (lane < 16) {
-        float* colp = slot(K, K) + m * CS;
-#pragma unroll
-        for (int c2 = 0; c2 < 8; ++c2)
-          *reinterpret_cast<float2*>(colp + 2 * c2) = make_float2(R16[2 * c2], R16[2 * c2 + 1]);
-      }
-    }
-    // (c) trailing update of this wave's tiles: B_IJ -= (D_K U_KI)^T U_KJ
-    if constexpr (K + 1 < NB) {
-      float dq[4];
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) dq[s4] = -Dv[K * 16 + 4 * s4 + q];
-      static_for<TS::N>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        constexpr int I = TS::g1(t), J = TS::g2(t);
-        if constexpr (I > K) {
-          floatx4 acc = A[t];
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(dq[s4] * slot(K, I)[m * CS + 4 * s4 + q],
-                                                        slot(K, J)[m * CS + 4 * s4 + q], acc, 0,
-                                                        0, 0);
-          A[t] = acc;
-          asm volatile("" ::: "memory");
-        }
-      });
-    }
-  });
-  const bool ok = __ballot(!okl) == 0;
-  if constexpr (R == 0) {
-    // (d) back substitution
-    block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);
-    // (e) un-permute: dim d = i*8 + K  <->  Xv[K*16 + i]
-    for (int d = lane; d < ld; d += 64) {
-      const float x = d < 16 * NB ? Xv[(d % NB) * 16 + d / NB] : 0.f;
-      xrow[d] = (d < k && ok) ? x : 0.f;
-    }
-  }
-  return ok;
-}
-
-// Wave R's part of completing one system: rhs blocks to LDS, YtY merge (fp64,
-// then one rounding), lambda * n on the diagonal, the workgroup panel LDL^T.
-template <int R, bool IMPLICIT, class AccT>
-__device__ __forceinline__ void wg_finish_and_solve(AccT (&tot)[WgTiles<R>::N][4],
-                                                    AccT (&bt)[WgTiles<R>::NRA], int64_t n_reg,
-                                                    float* lds, int k, float reg,
-                                                    const double* __restrict__ yty,
-                                                    float* __restrict__ xrow, int ld, int row,
-                                                    int32_t* __restrict__ status) {
-  typedef WgTiles<R> TS;
-  constexpr int NB = kWgNB;
-  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-#pragma unroll
-  for (int c = 0; c < TS::NR; ++c) {
-    AccT v = bt[c];
-    v += shfl_xor_t(v, 16);
-    v += shfl_xor_t(v, 32);
-    if (q == 0) lds[WgLds::RB + TS::gcol(c) * 16 + m] = m * NB + TS::gcol(c) < k ? (float)v : 0.f;
-  }
-  const float lam = (float)((double)reg * (double)n_reg);
-  floatx4 A[TS::N];
-  static_for<TS::N>([&](auto tc) {
-    constexpr int t = decltype(tc)::value;
-    constexpr int c1 = TS::g1(t), c2 = TS::g2(t);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int i, j;
-      tile_ij<NB>(c1, c2, r, i, j);
-      float v;
-      if constexpr (IMPLICIT) {
-        const int hi = i > j ? i : j, lo = i > j ? j : i;
-        v = (float)((double)tot[t][r] + yty[hi * (hi + 1) / 2 + lo]);
-      } else {
-        v = (float)tot[t][r];
-      }
-      if (i >= k || j >= k) v = 0.f;  // padded dims: identity rows/columns
-      if (c1 == c2 && i == j) v = (i < k) ? v + lam : 1.f;
-      A[t][r] = v;
-    }
-  });
-  const bool ok = wg_panel_solve<R>(A, lds, k, xrow, ld);
-  if (R == 0 && !ok && lane == 0) atomicCAS(status, 0, row + 1);
-}
-
 constexpr int kWgSub = Slot<10, 4>::SIZE;  // doubles per wave sub-slot (max over roles)
 constexpr int kWgSlot = 4 * kWgSub;
-
-template <int R, bool IMPLICIT>
-__device__ __forceinline__ void wg_gram_solve_task(
-    int task, const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
-    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
-    int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
-    int k, float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
-    int32_t* __restrict__ status, float* lds, const float* __restrict__ scal,
-    const uint32_t* __restrict__ Ysp, int32_t kp, int32_t zero_row) {
-  typedef WgTiles<R> TS;
-  floatx4 acc[TS::N];
-#pragma unroll
-  for (int t = 0; t < TS::N; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  float tot[TS::N][4], bt[TS::NRA];
-#pragma unroll
-  for (int c = 0; c < TS::NRA; ++c) bt[c] = 0.f;
-  int npos = 0;
-  int chunk, light;
-  decode_task(task, n_chunks, n_light, chunk, light);
-  int64_t pb, pe;
-  int row = -1;
-  if (chunk >= 0) {
-    pb = chunk_begin[chunk];
-    pe = chunk_end[chunk];
-  } else {
-    row = light_rows[light];
-    pb = row_ptr[row];
-    pe = row_ptr[row + 1];
-  }
-  int* st = reinterpret_cast<int*>(lds) + 192 * R;
-  float inv2;
-  if constexpr (IMPLICIT) {
-    const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
-    inv2 = ldexpf(1.f, -2 * e);
-    gram_accumulate_split<kWgNB, true, TS>(col, val, pb, pe, Y, ld, k, alpha, ldexpf(1.f, e), acc,
-                                           bt, npos, st);
-  } else {
-    const int ey = split_exponent(scal[0]), er = split_exponent(scal[1]);
-    inv2 = ldexpf(1.f, -2 * ey);
-    floatx4 accb[TS::NRA];
-#pragma unroll
-    for (int c = 0; c < TS::NRA; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    gram_accumulate_pre<TS>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row, ldexpf(1.f, er),
-                            (threadIdx.x & 15) * kWgNB, acc, accb, st);
-    rhs_from_tiles<TS>(accb, ldexpf(1.f, -ey - er), bt);
-  }
-#pragma unroll
-  for (int t = 0; t < TS::N; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
-  if (chunk >= 0) {
-    store_slot<TS::N, TS::NRA, float>(slots + (int64_t)chunk * kWgSlot + R * kWgSub, tot, bt,
-                                      npos);
-    return;
-  }
-  __syncthreads();  // staging area is reused by the solve
-  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  wg_finish_and_solve<R, IMPLICIT, float>(tot, bt, n_reg, lds, k, reg, yty, X + (int64_t)row * ld,
-                                          ld, row, status);
-}
-
-template <int R, bool IMPLICIT>
-__device__ __forceinline__ void wg_reduce_solve_task(int h, const int64_t* __restrict__ row_ptr,
-                                                     const int32_t* __restrict__ heavy_rows,
-                                                     const int32_t* __restrict__ slot_begin,
-                                                     const double* __restrict__ slots,
-                                                     float* __restrict__ X, int ld, int k, float reg,
-                                                     const double* __restrict__ yty,
-                                                     int32_t* __restrict__ status, float* lds) {
-  typedef WgTiles<R> TS;
-  const int row = heavy_rows[h];
-  double a64[TS::N][4], b64[TS::NRA];
-  zero_acc<TS::N, TS::NRA, double>(a64, b64);
-  int npos = 0;
-  for (int s = slot_begin[h]; s < slot_begin[h + 1]; ++s)
-    add_slot<TS::N, TS::NRA>(slots + (int64_t)s * kWgSlot + R * kWgSub, a64, b64, npos);
-  const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
-  wg_finish_and_solve<R, IMPLICIT, double>(a64, b64, n_reg, lds, k, reg, yty,
-                                           X + (int64_t)row * ld, ld, row, status);
-}
 
 template <int R>
 __device__ __forceinline__ void wg_yty_partial_task(const float* __restrict__ Y, int64_t n, int ld,
@@ -2323,38 +2046,6 @@ __device__ __forceinline__ void wg_yty_reduce_task(const double* __restrict__ sl
     else if (wv == 2) CALL(2);                                            \
     else CALL(3);                                                         \
   } while (0)
-
-template <bool IMPLICIT>
-__global__ __launch_bounds__(256, 2) void gram_solve_wg_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
-    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
-    int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
-    int k, float reg, float alpha, const double* __restrict__ yty, double* __restrict__ slots,
-    int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
-    int32_t kp, int32_t zero_row) {
-  __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
-#define CALL(R)                                                                                 \
-  wg_gram_solve_task<R, IMPLICIT>(blockIdx.x, row_ptr, col, val, light_rows, chunk_begin,      \
-                                  chunk_end, n_chunks, n_light, Y, X, ld, k, reg, alpha, yty, \
-                                  slots, status, lds, scal, Ysp, kp, zero_row)
-  ALS_WG_ROLES(CALL);
-#undef CALL
-}
-
-template <bool IMPLICIT>
-__global__ __launch_bounds__(256, 3) void reduce_solve_wg_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
-    const int32_t* __restrict__ slot_begin, const double* __restrict__ slots,
-    float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
-    int32_t* __restrict__ status) {
-  __shared__ __attribute__((aligned(16))) float lds[WgLds::SIZE];
-#define CALL(R)                                                                           \
-  wg_reduce_solve_task<R, IMPLICIT>(blockIdx.x, row_ptr, heavy_rows, slot_begin, slots, X, \
-                                    ld, k, reg, yty, status, lds)
-  ALS_WG_ROLES(CALL);
-#undef CALL
-}
 
 // Element-wise fp64 sum of the YtY task slots (fixed order: four interleaved
 // partial sums, then combined), so the final reduce reads one slot.
@@ -2424,23 +2115,12 @@ static size_t solve_table_bytes(int32_t k, int64_t n_src) {
   return align_up(sizeof(uint32_t) * (size_t)als_k_pad(k) * (size_t)((n_src > 0 ? n_src : 0) + 1));
 }
 
-// Dev switch for A/B timing: ALS_K128_PATH=wg selects the round-1 4-wave workgroup
-// solve for k in (64, 128] (default: W1, one wave per system).
-static bool wg_path() {
-  static const bool v = [] {
-    const char* e = getenv("ALS_K128_PATH");
-    return e && e[0] == 'w' && e[1] == 'g';
-  }();
-  return v;
-}
-
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src) {
   // 256 B of scale words | split table ((n_src + 1) x k_pad words, explicit) |
   // partial slots of the heavy-row chunks.  The first two sit at fixed offsets,
   // so calls over blocks that share Y_src can share one prep (phases).
-  const size_t sd = cn_for_k(k) == 8 ? std::max<size_t>(slot_doubles(k), kWgSlot) : slot_doubles(k);
   return 256 + ytyc_bytes(k) + solve_table_bytes(k, n_src) +
-         align_up(sizeof(double) * sd * (size_t)(n_chunks > 0 ? n_chunks : 0));
+         align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -2485,7 +2165,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const int zero_row = (int)n_src;
   if (phases & 4) {  // Y_src prep: max |Y_src|, split table (explicit) / YtY table (W1 implicit)
     ALS_HIP(hipMemsetAsync(scal_u, 0, sizeof(unsigned), st));
-    if (implicit && cn == 8 && !wg_path()) {
+    if (implicit && cn == 8) {
       yty_ctab_kernel<<<1, 64, 0, st>>>(yty_packed, ytyC);
       ALS_LAUNCH_CHECK();
     }
@@ -2533,20 +2213,6 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
   } while (0)
-#define ALS_SOLVE_WG_LAUNCH(IMP)                                                                  \
-  do {                                                                                            \
-    if (g1)                                                                                       \
-      gram_solve_wg_kernel<IMP><<<g1, 256, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,   \
-                                                    chunk_end, n_chunks, n_light, Y_src, X_dst,   \
-                                                    ld, k, reg, alpha, yty_packed, slots,         \
-                                                    status_dev, scal, Ysp, kp, zero_row);         \
-    ALS_LAUNCH_CHECK();                                                                           \
-    if (g2)                                                                                       \
-      reduce_solve_wg_kernel<IMP><<<g2, 256, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
-                                                      slots, X_dst, ld, k, reg, yty_packed,       \
-                                                      status_dev);                                \
-    ALS_LAUNCH_CHECK();                                                                           \
-  } while (0)
 #define ALS_SOLVE_W1_LAUNCH(IMP)                                                                  \
   do {                                                                                            \
     float* slots_f = reinterpret_cast<float*>(slots);                                             \
@@ -2569,18 +2235,15 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     if (cn == 1) ALS_SOLVE_LAUNCH(1, true);
     else if (cn == 2) ALS_SOLVE_LAUNCH(2, true);
     else if (cn == 4) ALS_SOLVE_LAUNCH(4, true);
-    else if (wg_path()) ALS_SOLVE_WG_LAUNCH(true);
     else ALS_SOLVE_W1_LAUNCH(true);
   } else {
     if (cn == 1) ALS_SOLVE_LAUNCH(1, false);
     else if (cn == 2) ALS_SOLVE_LAUNCH(2, false);
     else if (cn == 4) ALS_SOLVE_LAUNCH(4, false);
-    else if (wg_path()) ALS_SOLVE_WG_LAUNCH(false);
     else ALS_SOLVE_W1_LAUNCH(false);
   }
 #undef ALS_SOLVE_W1_LAUNCH
 #undef ALS_SOLVE_LAUNCH
-#undef ALS_SOLVE_WG_LAUNCH
   return ALS_OK;
 }
 

@@ -128,7 +128,7 @@ int oracle_half_sweep(const int64_t* indptr, const int32_t* indices, const float
     double* ata = (double*)malloc(sizeof(double) * tri);
     double* atb = (double*)malloc(sizeof(double) * k);
     double* da = (double*)malloc(sizeof(double) * k);
-#pragma omp for schedule(dynamic, 64)
+#pragma omp for schedule(dynamic, 1) /* heavy rows (millions of ratings) spread over threads */
     for (int32_t j = 0; j < n_rows; ++j) {
       memset(ata, 0, sizeof(double) * tri);
       memset(atb, 0, sizeof(double) * k);

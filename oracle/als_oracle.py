@@ -268,18 +268,24 @@ def rmse(U, V, umap, imap, u, i, r):
 # --------------------------------------------------------------------------
 # K5
 # --------------------------------------------------------------------------
-def topk(Q, V, top, batch=1024):
-    """Per row of Q: the `top` rows of V by score desc, ties by index asc (fp64 scores)."""
+def topk(Q, V, top, batch=64):
+    """Per row of Q: the `top` rows of V by score desc, ties by index asc (fp64 scores).
+    Exact: the rows scoring >= the row's top-th score (ties included) are ranked by
+    (score desc, index asc), so no full sort of the n_v scores is needed."""
     Q = np.asarray(Q, np.float32).astype(np.float64)
     V = np.asarray(V, np.float32).astype(np.float64)
     n_q, n_v = Q.shape[0], V.shape[0]
     t = min(top, n_v)
     idx = np.full((n_q, top), -1, dtype=np.int32)
     sc = np.full((n_q, top), -np.inf, dtype=np.float64)
+    if t == 0:
+        return idx, sc
     for s in range(0, n_q, batch):
         S = Q[s:s + batch] @ V.T
-        ar = np.broadcast_to(np.arange(n_v), S.shape)
-        order = np.lexsort((ar, -S), axis=1)[:, :t]
-        idx[s:s + batch, :t] = order
-        sc[s:s + batch, :t] = np.take_along_axis(S, order, axis=1)
+        kth = -np.partition(-S, t - 1, axis=1)[:, t - 1] if t < n_v else None
+        for j in range(S.shape[0]):
+            cand = np.nonzero(S[j] >= kth[j])[0] if kth is not None else np.arange(n_v)
+            order = cand[np.lexsort((cand, -S[j, cand]))][:t]
+            idx[s + j, :t] = order
+            sc[s + j, :t] = S[j, order]
     return idx, sc

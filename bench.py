@@ -12,22 +12,28 @@ all-gathers when N > 1.  N > 1 is weak scaling of this workload: rank r owns
 its own 162,541-user shard of one global dataset (same items); value = all
 ratings / max-over-ranks time.
 
-Secondary objects on the same line (BASELINE configs[3] and [4], the
-north-star scaling workload; `--no-big` skips them):
-  configs3: 1e9-rating power-law synthetic, 10M users x 1M items, rank 128,
-            explicit — STRONG scaling: the one global dataset is split over the N
+Secondary objects on the same line (the other BASELINE configs, each at full size;
+`--no-big` skips them):
+  configs2: configs[2], the same ML-25M data with implicitPrefs=True, alpha 40,
+            rank 128 (YtY Gram + confidence-weighted solves), ms/iter + roofline.
+  configs3: configs[3], 1e9-rating power-law synthetic, 10M users x 1M items, rank
+            128, explicit — STRONG scaling: the one global dataset is split over the N
             ranks by user range (each rank generates its range; ShardedALS routes
             ratings to row owners, RCCL all-gathers the factor halves), value =
             1e9 / iteration time.  N = 1 uses the single-GPU engine.
-  configs4: recommendForAllUsers top-10 and top-100 on those rank-128 factors,
-            over a user sample (262,144 users, split over the ranks; items all
-            1M), recs/s = sampled users / time.
+  configs4: configs[4], recommendForAllUsers top-10 and top-100 on those rank-128
+            factors over ALL 10M users x all 1M items (split over the ranks by user
+            range), recs/s = 10M / time.
 
-Also: `roofline` of the dominant kernel (timed with HIP events on its own
-stream; algorithmic bytes and MFMA flops per launch, PMC traffic and
-utilisation from the committed rocprofv3 summary), `topk_roofline`,
-`cpu_baseline` (the C port of Spark's per-row dspr + dppsv arithmetic,
-oracle/als_oracle.c, on the host cores, bounded sample).
+Every workload carries a roofline of its dominant kernel: algorithmic bytes and
+issued MFMA flops per launch over HIP-event launch times measured on the
+launching stream (`frac`), the same over the rocprofv3 kernel-trace average
+(`frac_rocprof`), and the PMC traffic / busy fractions / limiter of that
+workload's own profiled launches (profiles/pmc_summary.json, keyed by workload,
+kernel and grid size).  `cpu_baseline`: the C port of Spark's per-row dspr +
+dppsv arithmetic (oracle/als_oracle.c) on the host cores, bounded sample, with
+the Spark probe (java / pyspark) recorded.  `--only c1|c2|c3|c4` runs a single
+workload (profiling passes).
 """
 from __future__ import annotations
 
@@ -54,7 +60,7 @@ PEAK_FP32_TFLOPS = 157.3
 PEAK_F16_MFMA_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_summary.json")
-BIG_TOPK_SAMPLE = 262144
+TOPK_WARM_ROWS = 65536
 
 
 def dominant_kernel(k: int, implicit: bool) -> str:
@@ -78,128 +84,196 @@ def algorithmic_flops(nnz: int, n_solved: int, k: int) -> float:
 def mfma_issued_flops(nnz: int, n_solved: int, k: int, implicit: bool) -> float:
     """Matrix-core FLOPs the kernel actually issues per launch (what the MFMA pipes do):
     Gram: upper 16x16 tiles x 3 f16 MFMAs (split hi/lo) per 32 ratings (+ 2 rhs MFMAs
-    per dims-block, explicit); solve: fp32 16x16x4 trailing / block-row products."""
+    per dims-block, explicit); solve: 16x16 tile products of the block elimination."""
     cn = kp_of(k) // 16
     nt = cn * (cn + 1) // 2
     per32 = (3 * nt + (0 if implicit else 2 * cn)) * 16 * 16 * 32 * 2
     gram = nnz / 32.0 * per32
-    if cn == 8:   # W1: 28 Pm + 84 Schur tile products, 4 x 16x16x4 each
+    if cn == 8:   # W1: 28 Pm + 84 Schur tile products, 4 x 16x16x4 each (fp32-grade)
         solve = (28 + 84) * 4 * 16 * 16 * 4 * 2
-    else:         # panel LDL^T: trailing tile updates, 4 x 16x16x4 each
+    else:         # trailing tile updates, 4 x 16x16x4 each
         solve = sum((cn - 1 - K) * (cn - K) // 2 for K in range(cn)) * 4 * 16 * 16 * 4 * 2
     return gram + n_solved * solve
 
 
 def gather_bytes(nnz: int, n_rows: int, k: int) -> float:
-    """Algorithmic bytes of launch 1 of a half-sweep: per rating the gathered fp32
-    factor row (4k) + column index + rating (8 B); per solved row its output row (4k)
-    and row pointer (8 B).  Every byte counted once, no cache reuse assumed."""
+    """Algorithmic bytes of launch 1 of a half-sweep: per rating the gathered factor row
+    (4k) + column index + rating (8 B); per solved row its output row (4k) and row
+    pointer (8 B).  Every byte counted once, no cache reuse assumed."""
     return nnz * (4 * k + 8) + n_rows * (4 * k + 8)
 
 
-def load_pmc(kernel: str, prefix: bool = False):
-    """Per-launch rocprofv3 counters of `kernel` from the committed summary
-    (tools/gpu_pmc_r02.sh -> tools/pmc_fold.py), or None.  prefix=True: the first
-    kernel whose name starts with `kernel` (template arguments not known here)."""
+def _pmc_doc():
     try:
         with open(PMC_FILE) as f:
-            ks = json.load(f).get("kernels", {})
+            return json.load(f)
     except Exception:
+        return {}
+
+
+def load_pmc(workload: str, kernel: str, grid=None):
+    """Per-launch rocprofv3 counters of `kernel` in the committed profile of `workload`
+    (tools/gpu_pmc_r03.sh -> tools/pmc_fold.py; format 2: workloads -> kernel ->
+    all-dispatch averages + by_grid[grid threads]).  grid: the launch's grid size in
+    threads, which tells the item launch of a half-sweep from the user launch."""
+    ent = _pmc_doc().get("workloads", {}).get(workload, {}).get(kernel.replace(" ", ""))
+    if ent is None:
         return None
-    name = kernel.replace(" ", "")
-    if not prefix:
-        return ks.get(name)
-    hits = sorted(k_ for k_ in ks if k_.startswith(name))
-    return ks[hits[0]] if hits else None
+    if grid is not None:
+        return ent.get("by_grid", {}).get(str(int(grid)))
+    return ent
 
 
-def roofline(kernel: str, launch_ms: dict, nnz_rows: list, k: int, implicit: bool):
-    """launch_ms: {"item": ms, "user": ms} averages of launch 1 of each half-sweep."""
-    launch_s = sum(launch_ms.values()) * 1e-3
-    n_launch = len(launch_ms)
-    b = sum(gather_bytes(nz, rows, k) for nz, rows in nnz_rows)
-    f = sum(algorithmic_flops(nz, rows, k) for nz, rows in nnz_rows)
-    fm = sum(mfma_issued_flops(nz, rows, k, implicit) for nz, rows in nnz_rows)
-    hbm = b / launch_s / 1e9
-    mfma = fm / launch_s / 1e12
-    pmc = load_pmc(kernel)
-    out = {
-        "kernel": kernel,
-        "avg_launch_us": 1e6 * launch_s / n_launch,
-        "launch_ms": launch_ms,
-        "algorithmic_bytes_per_launch": b / n_launch,
+def _pmc_view(pmc, t_s):
+    """Counter view of one launch: traffic, busy fractions, limiter."""
+    if not pmc:
+        return None
+    keep = ("mfma_busy_frac", "valu_busy_frac", "fetch_bytes_x2", "write_bytes", "pmc_run_avg_ns",
+            "trace_avg_ns", "eff_clock_ghz", "dispatches")
+    v = {k_: pmc[k_] for k_ in keep if k_ in pmc}
+    traffic = pmc.get("fetch_bytes_x2", 0.0) + pmc.get("write_bytes", 0.0)
+    t_run = pmc.get("pmc_run_avg_ns")
+    if traffic > 0:
+        v["traffic_bytes"] = traffic
+        # counters and their own launch time come from the same profiled dispatches
+        tt = (t_run * 1e-9) if t_run else t_s
+        v["hbm_frac"] = traffic / tt / 1e9 / PEAK_HBM_GBS
+    busy = {"valu": pmc.get("valu_busy_frac"), "mfma": pmc.get("mfma_busy_frac"),
+            "hbm": v.get("hbm_frac")}
+    busy = {k_: x for k_, x in busy.items() if x is not None}
+    if busy:
+        v["limiter"] = max(busy, key=busy.get)
+        v["limiter_fracs"] = busy
+    return v
+
+
+def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool):
+    """Roofline of launch 1 of each half-sweep (the fused Gram + solve kernel).
+    launches: {"item"|"user": {"ms": HIP-event average on the launching stream,
+    "nnz": ratings, "rows": rows solved in the launch, "grid": grid threads}}.
+    achieved = algorithmic bytes (or issued flops) / event time; frac_rocprof uses the
+    rocprofv3 kernel-trace average of the same launch instead; traffic / busy
+    fractions / limiter come from that workload's PMC passes."""
+    out = {"kernel": kernel, "launches": {}}
+    tb = tf = tfa = te = tr = 0.0
+    traffic = 0.0
+    have_traffic = have_trace = True
+    busy_w = {}
+    for name, L in launches.items():
+        b = gather_bytes(L["nnz"], L["rows"], k)
+        fm = mfma_issued_flops(L["nnz"], L["rows"], k, implicit)
+        fa = algorithmic_flops(L["nnz"], L["rows"], k)
+        t = L["ms"] * 1e-3
+        ent = {"event_ms": L["ms"], "algorithmic_bytes": b, "hbm_gbs": b / t / 1e9,
+               "hbm_frac": b / t / 1e9 / PEAK_HBM_GBS, "mfma_issued_flops": fm,
+               "mfma_frac": fm / t / 1e12 / PEAK_F16_MFMA_TFLOPS,
+               "fp32_grade_tflops": fa / t / 1e12, "grid_threads": L["grid"]}
+        pv = _pmc_view(load_pmc(workload, kernel, L["grid"]), t)
+        if pv:
+            ent["pmc"] = pv
+            if pv.get("trace_avg_ns"):
+                ent["rocprof_ms"] = pv["trace_avg_ns"] * 1e-6
+                ent["hbm_frac_rocprof"] = b / (pv["trace_avg_ns"] * 1e-9) / 1e9 / PEAK_HBM_GBS
+                tr += pv["trace_avg_ns"] * 1e-9
+            else:
+                have_trace = False
+            if "traffic_bytes" in pv:
+                traffic += pv["traffic_bytes"]
+            else:
+                have_traffic = False
+            for k_, x in pv.get("limiter_fracs", {}).items():
+                busy_w[k_] = busy_w.get(k_, 0.0) + x * t
+        else:
+            have_trace = have_traffic = False
+        out["launches"][name] = ent
+        tb += b
+        tf += fm
+        tfa += fa
+        te += t
+    n = len(launches)
+    hbm = tb / te / 1e9
+    mf = tf / te / 1e12
+    out.update({
+        "avg_launch_us": 1e6 * te / n,
+        "algorithmic_bytes_per_launch": tb / n,
         "hbm_view": {"achieved_gbs": hbm, "peak_gbs": PEAK_HBM_GBS, "frac": hbm / PEAK_HBM_GBS},
-        "mfma_view": {"issued_flops_per_launch": fm / n_launch, "achieved_tflops": mfma,
-                      "peak_tflops": PEAK_F16_MFMA_TFLOPS,
-                      "frac": mfma / PEAK_F16_MFMA_TFLOPS,
+        "mfma_view": {"issued_flops_per_launch": tf / n, "achieved_tflops": mf,
+                      "peak_tflops": PEAK_F16_MFMA_TFLOPS, "frac": mf / PEAK_F16_MFMA_TFLOPS,
                       "note": "f16 matrix-core flops issued (split-f16 Gram: 3 MFMAs per "
-                              "fp32-grade product) + fp32 16x16x4 solve flops"},
-        "fp32_grade_view": {"algorithmic_flops_per_launch": f / n_launch,
-                            "achieved_tflops": f / launch_s / 1e12,
-                            "peak_tflops": PEAK_FP32_TFLOPS},
-    }
-    traffic = None
-    if pmc:
-        t = pmc.get("fetch_bytes_x2", 0.0) + pmc.get("write_bytes", 0.0)
-        traffic = t if t > 0 else None
-        out["pmc"] = {k_: pmc[k_] for k_ in ("mfma_busy_frac", "valu_busy_frac", "fetch_bytes_x2",
-                                             "write_bytes", "pmc_run_avg_ns", "eff_clock_ghz")
-                      if k_ in pmc}
-        out["pmc"]["source"] = os.path.relpath(PMC_FILE, ROOT)
-        if traffic:
-            tb = traffic / (1e-6 * out["avg_launch_us"]) / 1e9
-            out["pmc_traffic_view"] = {"bytes_per_launch": traffic, "achieved_gbs": tb,
-                                       "peak_gbs": PEAK_HBM_GBS, "frac": tb / PEAK_HBM_GBS,
-                                       "note": "L2 memory-side bytes (FETCH_SIZE x2 + WRITE_SIZE); "
-                                               "below the algorithmic bytes = factor rows "
-                                               "re-read from L2 / Infinity Cache"}
-        busy = {"valu": pmc.get("valu_busy_frac"), "mfma": pmc.get("mfma_busy_frac"),
-                "hbm": (traffic / (1e-6 * out["avg_launch_us"]) / 1e9 / PEAK_HBM_GBS)
-                if traffic else None}
-        busy = {k_: v for k_, v in busy.items() if v is not None}
-        if busy:
-            out["limiter"] = max(busy, key=busy.get)
-            out["limiter_fracs"] = busy
-    # contract: bound in {hbm, mfma}; the larger of the two live fractions
-    bound = "hbm" if out["hbm_view"]["frac"] >= out["mfma_view"]["frac"] else "mfma"
+                              "fp32-grade product) + the solve's tile products"},
+        "fp32_grade_view": {"algorithmic_flops_per_launch": tfa / n,
+                            "achieved_tflops": tfa / te / 1e12, "peak_tflops": PEAK_FP32_TFLOPS},
+    })
+    busy = {k_: x / te for k_, x in busy_w.items()} if busy_w else {}
+    if busy:
+        out["limiter"] = max(busy, key=busy.get)
+        out["limiter_fracs"] = busy
+    # bound (contract: hbm | mfma): the larger counter-measured fraction of the two when
+    # the counters exist, else the larger algorithmic view
+    if "hbm" in busy and "mfma" in busy:
+        bound = "hbm" if busy["hbm"] >= busy["mfma"] else "mfma"
+    else:
+        bound = "hbm" if out["hbm_view"]["frac"] >= out["mfma_view"]["frac"] else "mfma"
     view = out["hbm_view"] if bound == "hbm" else out["mfma_view"]
     out.update({"bound": bound,
                 "achieved": view["achieved_gbs"] if bound == "hbm" else view["achieved_tflops"],
                 "peak": PEAK_HBM_GBS if bound == "hbm" else PEAK_F16_MFMA_TFLOPS,
                 "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
-                "frac": view["frac"], "traffic": traffic})
+                "frac": view["frac"],
+                "traffic": traffic / n if (have_traffic and traffic > 0) else None})
+    if have_trace and tr > 0:
+        out["frac_rocprof"] = (tb / tr / 1e9 / PEAK_HBM_GBS) if bound == "hbm" else \
+            (tf / tr / 1e12 / PEAK_F16_MFMA_TFLOPS)
+        out["rocprof_avg_launch_us"] = 1e6 * tr / n
     return out
 
 
-def topk_roofline(n_q: int, n_v: int, k: int, ms: float, top: int):
-    useful = 2.0 * n_q * n_v * k
-    kq = max(32, kp_of(k))  # topk_kq (csrc/topk.hip): dims padded to 32/64/128
-    issued = 3.0 * 2.0 * n_q * n_v * kq
-    s = ms * 1e-3
-    out = {"kernel": "topk_split_kernel", "top": top, "n_q": n_q, "n_v": n_v, "rank": k,
-           "ms": ms, "recs_per_s": n_q / s,
-           "useful_fp32_grade_tflops": useful / s / 1e12,
-           "issued_f16_mfma_tflops": issued / s / 1e12,
-           "mfma_frac": issued / s / 1e12 / PEAK_F16_MFMA_TFLOPS,
-           "bound": "mfma", "unit": "TFLOP/s"}
-    # the launched variant (csrc/topk.hip als_topk): <NK, row groups, list kind, 0>
-    nk = kq // 32
+def topk_variant(k: int, top: int) -> str:
+    """The kernel als_topk launches (csrc/topk.hip): <NK, row groups, list kind, 0>."""
+    nk = max(32, kp_of(k)) // 32
     if top <= 16:
         rg, tr = 2, (8 if top <= 8 else (12 if top <= 12 else 16))
     elif top <= 128:  # quad register lists, one row group
         rg, tr = 1, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
     else:
-        rg, tr = None, 0
-    out["kernel"] = f"topk_split_kernel<{nk},{rg if rg else '?'},{tr},0>"
-    pmc = load_pmc(out["kernel"]) if rg else None
-    if pmc:
-        out["pmc"] = {k_: pmc.get(k_) for k_ in ("mfma_busy_frac", "valu_busy_frac",
-                                                 "pmc_run_avg_ns")}
-        busy = {"valu": pmc.get("valu_busy_frac"), "mfma": pmc.get("mfma_busy_frac")}
-        busy = {k_: v for k_, v in busy.items() if v is not None}
-        if busy:
-            out["limiter"] = max(busy, key=busy.get)
+        return f"topk_split_kernel<{nk},?,0,0>"
+    return f"topk_split_kernel<{nk},{rg},{tr},0>"
+
+
+def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int):
+    useful = 2.0 * n_q * n_v * k
+    kq = max(32, kp_of(k))  # topk_kq (csrc/topk.hip): dims padded to 32/64/128
+    issued = 3.0 * 2.0 * n_q * n_v * kq
+    s = ms * 1e-3
+    kern = topk_variant(k, top)
+    out = {"kernel": kern, "top": top, "n_q": n_q, "n_v": n_v, "rank": k,
+           "ms": ms, "recs_per_s": n_q / s,
+           "useful_fp32_grade_tflops": useful / s / 1e12,
+           "issued_f16_mfma_tflops": issued / s / 1e12,
+           "bound": "mfma", "achieved": issued / s / 1e12, "peak": PEAK_F16_MFMA_TFLOPS,
+           "unit": "TFLOP/s", "frac": issued / s / 1e12 / PEAK_F16_MFMA_TFLOPS,
+           "algorithmic_bytes": 4.0 * (n_q + n_v) * k + 8.0 * n_q * top}
+    pv = _pmc_view(load_pmc(workload, kern), s)
+    if pv:
+        out["pmc"] = pv
+        out["traffic"] = pv.get("traffic_bytes")
+        if pv.get("trace_avg_ns"):
+            out["frac_rocprof"] = issued / (pv["trace_avg_ns"] * 1e-9) / 1e12 / PEAK_F16_MFMA_TFLOPS
+        if "limiter" in pv:
+            out["limiter"] = pv["limiter"]
     return out
+
+
+def _probe_spark():
+    """is Spark runnable on this host?  (java on PATH, pyspark importable)"""
+    import importlib.util
+    import shutil
+    java = shutil.which("java")
+    try:
+        pys = importlib.util.find_spec("pyspark") is not None
+    except Exception:
+        pys = False
+    return {"java": java, "pyspark": pys}
 
 
 def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.0,
@@ -209,6 +283,10 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
     import numpy as np
     from oracle import c_oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except Exception:
+        affinity = None
     U = core.U[:, :rank].contiguous().cpu().numpy()
     V = core.V[:, :rank].contiguous().cpu().numpy()
     total_t = 0.0
@@ -233,25 +311,93 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
             target = int(rate * budget_s / 2)
         total_t += block.nnz / rate
         sample_desc.append(f"{name} side: first {nrow} rows ({nz} ratings) in {dt:.2f}s")
+    probe = _probe_spark()
     return {"value": core.nnz / total_t, "unit": "ratings/s", "cores": threads, "kind": "port",
-            "sample": "oracle/als_oracle.c (Spark dspr+dppsv restated, fp64, OpenMP) on a row "
-                      "prefix of each side; " + "; ".join(sample_desc)
-                      + "; full-iteration time extrapolated as sum over sides of nnz/rate"}
+            "host_cores": os.cpu_count(), "affinity_cores": affinity, "spark_probe": probe,
+            "sample": "oracle/als_oracle.c (Spark dspr+dppsv restated, fp64, OpenMP, "
+                      f"{threads} threads) on a row prefix of each side; "
+                      + "; ".join(sample_desc)
+                      + "; full-iteration time extrapolated as sum over sides of nnz/rate; "
+                      + ("Spark not runnable here (java: %s, pyspark importable: %s)"
+                         % (probe["java"] or "absent", probe["pyspark"]))}
 
 
 def _timed_topk(Q, n_q, V, n_v, k, top):
-    E.topk_rows(Q, n_q, V, n_v, k, top)  # warm (workspace, split table)
+    """recommendForAll over all n_q rows: warmed on a small prefix, then one timed call
+    bracketed by HIP events on the launching stream."""
+    E.topk_rows(Q, min(n_q, TOPK_WARM_ROWS), V, n_v, k, top)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    E.topk_rows(Q, n_q, V, n_v, k, top)
+    idx, sc = E.topk_rows(Q, n_q, V, n_v, k, top)
     e1.record()
     torch.cuda.synchronize()
+    del idx, sc
     return e0.elapsed_time(e1)
 
 
-def big_single(args, dev):
-    """configs[3] (N = 1) and configs[4] on its factors."""
+def _half_sweep_timed(core, block, Y, X, k, reg, imp, alpha, yty, ev=None):
+    """solve_half in its phases, launch 1 bracketed by events (ev = (start, end))."""
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, 12)
+    if ev is not None:
+        ev[0].record()
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, 1)
+    if ev is not None:
+        ev[1].record()
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, 2)
+
+
+def _iteration(core, k, reg, imp, alpha, evs=None):
+    """One ALS iteration in Spark's order (ALS.train loop): items from users, then users
+    from items; implicit: YtY of the source side before each half-sweep (computeYtY)."""
+    yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
+    _half_sweep_timed(core, core.item_block, core.U, core.V, k, reg, imp, alpha, yty,
+                      evs[0:2] if evs else None)
+    yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
+    _half_sweep_timed(core, core.user_block, core.V, core.U, k, reg, imp, alpha, yty,
+                      evs[2:4] if evs else None)
+
+
+def _launch1_grid(block) -> int:
+    return 64 * (block.n_chunks + block.n_light)
+
+
+def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
+    """warmup + `steps` timed iterations from the seeded start; per-iteration wall time
+    and the event times of launch 1 of each half-sweep -> (ms_per_iter, roofline)."""
+    core.init_factors(k, seed=5)
+    core.status.zero_()
+    for _ in range(warmup):
+        _iteration(core, k, reg, imp, alpha)
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s in range(steps):
+        _iteration(core, k, reg, imp, alpha, evs[s])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    core.check_status()
+    ib, ub = core.item_block, core.user_block
+    launches = {
+        "item": {"ms": sum(e[0].elapsed_time(e[1]) for e in evs) / steps, "nnz": ib.nnz,
+                 "rows": ib.n_light, "grid": _launch1_grid(ib)},
+        "user": {"ms": sum(e[2].elapsed_time(e[3]) for e in evs) / steps, "nnz": ub.nnz,
+                 "rows": ub.n_light, "grid": _launch1_grid(ub)}}
+    return 1e3 * dt, roofline(workload, dominant_kernel(k, imp), launches, k, imp)
+
+
+def configs2(core, args):
+    """BASELINE configs[2]: the ML-25M shape, implicitPrefs=True alpha=40, rank 128."""
+    k, alpha = 128, 40.0
+    ms, roof = timed_fit(core, "configs2", k, args.reg, True, alpha, args.steps, args.warmup)
+    return {"workload": "ml25m implicit alpha=40 ALS rank 128 (BASELINE configs[2]), 1 GPU",
+            "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz, "rank": k,
+            "alpha": alpha, "ratings_per_s": core.nnz / (ms * 1e-3), "ms_per_iter": ms,
+            "steps": args.steps, "warmup": args.warmup, "roofline": roof}
+
+
+def big_single(args, dev, want_c3=True, want_c4=True):
+    """configs[3] (N = 1) and configs[4] on its factors (all 10M users)."""
     k = 128
     t0 = time.perf_counter()
     u, i, r = D.big_config("big1b", device=dev)
@@ -263,40 +409,46 @@ def big_single(args, dev):
     t_build = time.perf_counter() - t0
     del u, i, r
     torch.cuda.empty_cache()
-    core.init_factors(k, seed=5)
-    core.status.zero_()
     steps = max(1, min(args.steps, args.big_steps))
-    core.iterate(args.reg)  # warmup
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        core.iterate(args.reg)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    core.check_status()
-    res = {"workload": "big1b explicit ALS rank 128 (BASELINE configs[3]), 1 GPU",
-           "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz, "rank": k,
-           "ratings_per_s": core.nnz / dt, "ms_per_iter": 1e3 * dt, "steps": steps,
-           "warmup": 1, "datagen_s": t_gen, "build_s": t_build, "scaling": "strong",
-           "n_gpus": 1}
-    s = min(BIG_TOPK_SAMPLE, core.n_users)
-    Q = core.U[:s].contiguous()
-    c4 = {"workload": f"recommendForAllUsers on configs[3] factors (BASELINE configs[4]); "
-                      f"sample: first {s} users (dense order) x all {core.n_items} items",
-          "rank": k}
-    for top in (10, 100):
-        ms = _timed_topk(Q, s, core.V, core.n_items, k, top)
-        c4[f"top{top}_recs_per_s"] = s / (ms * 1e-3)
-        c4[f"top{top}_ms"] = ms
-        c4[f"top{top}_roofline"] = topk_roofline(s, core.n_items, k, ms, top)
+    c3 = c4 = None
+    if want_c3:
+        ms, roof = timed_fit(core, "configs3", k, args.reg, False, 1.0, steps, 1)
+        c3 = {"workload": "big1b explicit ALS rank 128 (BASELINE configs[3]), 1 GPU",
+              "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz, "rank": k,
+              "ratings_per_s": core.nnz / (ms * 1e-3), "ms_per_iter": ms, "steps": steps,
+              "warmup": 1, "datagen_s": t_gen, "build_s": t_build, "scaling": "strong",
+              "n_gpus": 1, "roofline": roof,
+              "schedule": {"item": [core.item_block.n_light, core.item_block.n_heavy,
+                                    core.item_block.n_chunks],
+                           "user": [core.user_block.n_light, core.user_block.n_heavy,
+                                    core.user_block.n_chunks]}}
+    else:
+        core.init_factors(k, seed=5)
+        for _ in range(2):
+            core.iterate(args.reg)
+        torch.cuda.synchronize()
+    if want_c4:
+        c4 = {"workload": f"recommendForAllUsers on the configs[3] factors (BASELINE "
+                          f"configs[4]): all {core.n_users} users x all {core.n_items} items",
+              "rank": k, "n_users": core.n_users, "n_items": core.n_items}
+        for top in (10, 100):
+            ms = _timed_topk(core.U, core.n_users, core.V, core.n_items, k, top)
+            c4[f"top{top}_recs_per_s"] = core.n_users / (ms * 1e-3)
+            c4[f"top{top}_ms"] = ms
+            c4[f"top{top}_roofline"] = topk_roofline(f"configs4_top{top}", core.n_users,
+                                                     core.n_items, k, ms, top)
     del core
     torch.cuda.empty_cache()
-    return res, c4
+    return c3, c4
 
 
 def run_single(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if args.only in ("c3", "c4"):
+        c3, c4 = big_single(args, dev, args.only == "c3", args.only == "c4")
+        print(json.dumps({"configs3": c3} if c3 else {"configs4": c4}), file=OUT, flush=True)
+        return
     t0 = time.perf_counter()
     u, i, r = D.synthetic_config(args.config, device=dev)
     torch.cuda.synchronize()
@@ -308,51 +460,15 @@ def run_single(args):
     torch.cuda.synchronize()
     build_ms = ev0.elapsed_time(ev1)
     del u, i, r
+    if args.only == "c2":
+        print(json.dumps({"configs2": configs2(core, args)}), file=OUT, flush=True)
+        return
     k = args.rank
-    core.init_factors(k, seed=5)
-    core.status.zero_()
-    ib, ub = core.item_block, core.user_block
     imp, alpha = args.implicit, args.alpha
-
-    def iteration(evs=None):
-        # Spark order: items from users, then users from items (ALS.train loop);
-        # implicit: YtY of the source side before each half-sweep (computeYtY)
-        yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
-        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 12)
-        if evs is not None:
-            evs[0].record()
-        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
-        if evs is not None:
-            evs[1].record()
-        E.solve_half(ib, core.U, core.V, k, args.reg, imp, alpha, yty, core.status, core.ws, 2)
-        yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
-        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 12)
-        if evs is not None:
-            evs[2].record()
-        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 1)
-        if evs is not None:
-            evs[3].record()
-        E.solve_half(ub, core.V, core.U, k, args.reg, imp, alpha, yty, core.status, core.ws, 2)
-
-    for _ in range(args.warmup):
-        iteration()
-    torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    t_start = time.perf_counter()
-    for s in range(args.steps):
-        iteration(evs[s])
-    torch.cuda.synchronize()
-    t_total = time.perf_counter() - t_start
-    core.check_status()
-    ms_per_step = 1000.0 * t_total / args.steps
-    value = core.nnz / (t_total / args.steps)
-
-    # roofline of the dominant kernel (launch 1 of each half-sweep, HIP events on its stream)
-    item_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    user_ms = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    roof = roofline(dominant_kernel(k, imp), {"item": item_ms, "user": user_ms},
-                    [(ib.nnz, ib.n_light), (ub.nnz, ub.n_light)], k, imp)
-
+    wl = "configs2" if (imp and k == 128) else "configs1"
+    ms_per_step, roof = timed_fit(core, wl, k, args.reg, imp, alpha, args.steps, args.warmup)
+    value = core.nnz / (ms_per_step * 1e-3)
+    ib, ub = core.item_block, core.user_block
     # top-10 recommendations for all users (K5)
     topk_ms = _timed_topk(core.U, core.n_users, core.V, core.n_items, k, 10)
     mode = f"implicit alpha={alpha:g}" if imp else "explicit"
@@ -378,7 +494,8 @@ def run_single(args):
         "roofline": roof,
         "topk10_recs_per_s": core.n_users / (topk_ms * 1e-3),
         "topk10_ms": topk_ms,
-        "topk_roofline": topk_roofline(core.n_users, core.n_items, k, topk_ms, 10),
+        "topk_roofline": topk_roofline("configs1_top10", core.n_users, core.n_items, k, topk_ms,
+                                       10),
         "csr_build_ms": build_ms,
         "datagen_s": t_gen,
         "schedule": {"item": [ib.n_light, ib.n_heavy, ib.n_chunks],
@@ -391,6 +508,11 @@ def run_single(args):
         out["cpu_baseline"] = cpu_baseline(core, k, args.reg, args.cpu_budget, imp, alpha)
     else:
         out["cpu_baseline"] = None
+    if args.big and not imp and args.config == "ml25m":
+        try:
+            out["configs2"] = configs2(core, args)
+        except Exception as e:  # the primary line must still print
+            out["configs2"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     del core, ib, ub
     torch.cuda.empty_cache()
     if args.big:
@@ -450,23 +572,28 @@ def big_distributed(args, dev, rank, world):
            "ratings_per_s": sh.nnz / (t / steps), "ms_per_iter": 1e3 * t / steps,
            "steps": steps, "warmup": 1, "datagen_s": t_gen, "build_s": t_build,
            "scaling": "strong", "n_gpus": world, "chunks": sh.users.chunks}
-    # configs[4]: each rank scores its share of the user sample against the replicated V
-    s_loc = min(BIG_TOPK_SAMPLE // world, sh.users.chunk_rows(rank, 0))
+    # configs[4]: each rank scores its own users (every chunk of its range) against the
+    # replicated V; time = max over ranks
     Vd = sh._dense(False)
-    Q = sh.U_loc[0, :s_loc].contiguous()
-    c4 = {"workload": f"recommendForAllUsers on configs[3] factors (BASELINE configs[4]); "
-                      f"sample: {s_loc} users per rank x {world} ranks x all {sh.n_items} items",
-          "rank": k}
+    cs = sh.users.cstarts[rank]
+    c4 = {"workload": f"recommendForAllUsers on the configs[3] factors (BASELINE configs[4]): "
+                      f"all {sh.n_users} users (each rank its own range) x all {sh.n_items} "
+                      "items", "rank": k}
     for top in (10, 100):
-        E.topk_rows(Q, s_loc, Vd, sh.n_items, k, top)
+        E.topk_rows(sh.U_loc[0], min(sh.users.chunk_rows(rank, 0), TOPK_WARM_ROWS), Vd,
+                    sh.n_items, k, top)
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        E.topk_rows(Q, s_loc, Vd, sh.n_items, k, top)
+        for c in range(sh.users.chunks):
+            n_c = int(cs[c + 1] - cs[c])
+            if n_c > 0:
+                idx, sc = E.topk_rows(sh.U_loc[c], n_c, Vd, sh.n_items, k, top)
+                del idx, sc
         torch.cuda.synchronize()
         dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-        c4[f"top{top}_recs_per_s"] = s_loc * world / float(dt)
+        c4[f"top{top}_recs_per_s"] = sh.n_users / float(dt)
         c4[f"top{top}_ms"] = 1e3 * float(dt)
     return res, c4
 
@@ -557,9 +684,13 @@ def main():
                     help="timed iterations of configs[3] (at most --steps)")
     ap.add_argument("--chunks", type=int, default=None,
                     help="row chunks per rank for the overlapped all-gathers (N>1)")
+    ap.add_argument("--only", choices=("c1", "c2", "c3", "c4"), default=None,
+                    help="profiling runs: only this workload (c4 fits c3 untimed first)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the sharded (RCCL) code path even with one rank")
     args = ap.parse_args()
+    if args.only == "c1":
+        args.big, args.cpu_baseline = False, False
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.force_dist:
         run_distributed(args)
     else:

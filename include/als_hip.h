@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 3
+#define ALS_ABI_VERSION 4
 
 #define ALS_OK 0
 #define ALS_EINVAL (-1)   /* bad argument (shape, null pointer, rank) */
@@ -117,10 +117,17 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * across calls, issue them in that order on one stream with the same
  * workspace.  Blocks that share Y_src (row chunks of one half-sweep) may share
  * one bit-2 prep: it sits at a fixed workspace offset (size the workspace for
- * the largest n_chunks). */
+ * the largest n_chunks).
+ * n_light_primal (0 <= n_light_primal <= n_light): the first n_light_primal light
+ * rows are solved on the k x k normal equations above; the remaining light rows
+ * (the tail of the longest-first light list) must have <= 64 ratings and are
+ * solved through the equivalent n x n dual system (push-through identity
+ * (Y^T Y + lambda n I)^-1 Y^T r = Y^T (Y Y^T + lambda n I)^-1 r), allowed for
+ * explicit feedback, 64 < k <= 128, reg > 0 only.  n_light_primal = n_light
+ * keeps every row on the primal path. */
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src);
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
-                   const int32_t* light_rows, int32_t n_light,
+                   const int32_t* light_rows, int32_t n_light, int32_t n_light_primal,
                    const int32_t* heavy_rows, const int32_t* heavy_slot_begin, int32_t n_heavy,
                    const int32_t* chunk_row, const int64_t* chunk_begin, const int64_t* chunk_end,
                    int32_t n_chunks,

@@ -1284,11 +1284,13 @@ __device__ __forceinline__ half8v dup_lo(const half8v& v) {
   return __builtin_shufflevector(v, v, 4, 5, 6, 7, 4, 5, 6, 7);
 }
 
-// NB = 8 (rank 65-128, W1 kernels) or 4 (rank 33-64, explicit gram_solve_kernel).
+// NB = 8 (rank 65-128, W1 kernels), 4 (rank 33-64, explicit gram_solve_kernel) or
+// 2 / 4 (the n x n dual systems of short rows, gram_solve_dual_kernel).  Returns
+// whether every pivot was positive and the solution finite; xcol[c] on lane (q, m)
+// = solution entry of variable (block c, index m), every row group q.
 template <int NB, bool SPLIT = kW1SplitSchur<NB>>
-__device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
-                                         float* __restrict__ lds, int k,
-                                         float* __restrict__ xrow, int ld) {
+__device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
+                                           float* __restrict__ lds, int k, float (&xcol)[NB]) {
   using L = W1LdsT<NB>;
   constexpr int CS = L::CS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
@@ -1435,7 +1437,6 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
     }
   });
   // back substitution x_K = z_K + sum_{J>K} Pm_KJ x_J (column layout)
-  float xcol[NB];
   xcol[NB - 1] = zcol[NB - 1];
   static_for<NB - 1>([&](auto kc) {
     constexpr int K = NB - 2 - decltype(kc)::value;
@@ -1458,8 +1459,18 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
   bool fin = true;
 #pragma unroll
   for (int c = 0; c < NB; ++c) fin = fin && (xcol[c] - xcol[c] == 0.f);
-  const bool ok = dmin > 0.f && __ballot(!fin) == 0;
-  // un-permute: dim d = i * 8 + c  <->  block c, index i = lane m
+  return dmin > 0.f && __ballot(!fin) == 0;
+}
+
+// w1_solve_x, then the solution row written un-permuted: dim d = i * NB + c <->
+// block c, index i = lane m; dims in [k, ld) written as zero.
+template <int NB, bool SPLIT = kW1SplitSchur<NB>>
+__device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
+                                         float* __restrict__ lds, int k,
+                                         float* __restrict__ xrow, int ld) {
+  float xcol[NB];
+  const bool ok = w1_solve_x<NB, SPLIT>(A, bcol, lds, k, xcol);
+  const int lane = threadIdx.x & 63, m = lane & 15;
   if (lane < 16) {
 #pragma unroll
     for (int c = 0; c < NB; ++c) {
@@ -1897,6 +1908,183 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
                                                X + (int64_t)row * ld, ld, row, status);
 }
 
+// ---------------------------------------------------------------------------
+// Short explicit rows at 64 < k <= 128: the n x n dual system.
+// For a row with n <= 64 ratings r_j on the factor rows y_j (Y_S = n x k):
+//   x = (Y_S^T Y_S + lambda n I)^-1 Y_S^T r  =  Y_S^T (Y_S Y_S^T + lambda n I)^-1 r
+// (push-through identity (Y^T Y + c I) Y^T = Y^T (Y Y^T + c I); both systems are
+// SPD for lambda n > 0).  So x is the solution of Spark's CholeskySolver on the
+// k x k normal equations, obtained through an n x n system: for n < k the
+// k(k+1)/2-entry Gram and the k^3/3 factorisation become n(n+1)/2 k-dim inner
+// products and an n^3/3 one (n = 64, k = 128: 1/2 the Gram, 1/8 the solve).
+// Variables: rating j <-> (block c = j % NB, index i = j / NB) — the dim
+// permutation of the primal kernels — so w1_solve_x consumes the Gram tiles as
+// the MFMAs leave them and pads ratings j >= n the way it pads dims.
+//  * Gram G = 2^2ey Y_S Y_S^T on v_mfma_f32_16x16x32_f16 from the split table
+//    (hi | lo words of 2^ey Y): MFMA K = dims, 4 k-steps of 32; operand (c, s) on
+//    lane (q, m) = dims 32s + 8q .. +7 of rating m * NB + c; hi.hi + hi.lo + lo.hi
+//    per tile per k-step (fp32-grade products, as the primal Gram).
+//  * solve: w1_solve_x<NB> (fp32 MFMA tile products), z_j on the lanes of block c.
+//  * x = Y_S^T z from the same rows re-gathered (L2-hot): a split word is the f16
+//    pair (hi, lo) of one entry, so v_dot2_f32_f16 against (z_hi, z_hi) and
+//    (z_lo, z_lo) (z split after a power-of-two scale) accumulates (hi + lo) z in
+//    fp32; summed over the 16 lanes of a row group.
+// NB = 2 for n <= 32, 4 for n <= 64: a wave-uniform branch of one kernel.
+constexpr int kDualMaxRatings = 64;
+
+template <int NB>
+__device__ __forceinline__ void dual_gather(uint32_t (&w)[NB][4][8], const int (&cc)[NB],
+                                            const uint32_t* __restrict__ Ysp) {
+  const int q = (threadIdx.x & 63) >> 4;
+#pragma unroll
+  for (int c = 0; c < NB; ++c)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t* p = Ysp + (uint64_t)(uint32_t)cc[c] * 128u + 32 * s + 8 * q;
+      const uint4 a = *reinterpret_cast<const uint4*>(p);
+      const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
+      w[c][s][0] = a.x; w[c][s][1] = a.y; w[c][s][2] = a.z; w[c][s][3] = a.w;
+      w[c][s][4] = b.x; w[c][s][5] = b.y; w[c][s][6] = b.z; w[c][s][7] = b.w;
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ void dual_row(int row, int64_t pb, int n,
+                                         const int32_t* __restrict__ col,
+                                         const float* __restrict__ val,
+                                         const uint32_t* __restrict__ Ysp, int zero_row, int ey,
+                                         float reg, float* __restrict__ xrow, int ld,
+                                         float* __restrict__ lds, int32_t* __restrict__ status) {
+  constexpr int NT = NB * (NB + 1) / 2;
+  typedef FullTiles<NB> TS;
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  // lane j < n loads rating j; operand block c of lane (q, m) is rating m * NB + c
+  const int cj = lane < n ? col[pb + lane] : zero_row;
+  const float rj = lane < n ? val[pb + lane] : 0.f;
+  int cc[NB];
+  float rc[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) {
+    cc[c] = __shfl(cj, m * NB + c);
+    rc[c] = __shfl(rj, m * NB + c);
+  }
+  floatx4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  {
+    uint32_t w[NB][4][8];
+    dual_gather<NB>(w, cc, Ysp);
+    static_for<4>([&](auto sc) {
+      constexpr int s = decltype(sc)::value;
+      uint32_t hi[NB][4], lo[NB][4];
+#pragma unroll
+      for (int c = 0; c < NB; ++c)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          hi[c][p] = __builtin_amdgcn_perm(w[c][s][2 * p + 1], w[c][s][2 * p], 0x05040100u);
+          lo[c][p] = __builtin_amdgcn_perm(w[c][s][2 * p + 1], w[c][s][2 * p], 0x07060302u);
+        }
+      static_for<NT>([&](auto ti) {
+        constexpr int t = decltype(ti)::value;
+        constexpr int a = TS::l1(t), b = TS::l2(t);
+        const half8v ha = as_h8(hi[a]), hb = as_h8(hi[b]);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, as_h8(lo[b]), acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(lo[a]), hb, acc[t], 0, 0, 0);
+      });
+    });
+  }
+  // (2^2ey G + 2^2ey lambda n I) z = 2^2ey r; ratings j >= n: identity rows, rhs 0
+  const float inv = ldexpf(1.f, 2 * ey);
+  const float lam = (float)((double)reg * (double)n) * inv;
+  static_for<NT>([&](auto tc) {
+    constexpr int t = decltype(tc)::value;
+    constexpr int c1 = TS::l1(t), c2 = TS::l2(t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int i, j;
+      tile_ij<NB>(c1, c2, r, i, j);
+      const bool pad = (i >= n) | (j >= n);
+      float v = pad ? 0.f : acc[t][r];
+      if constexpr (c1 == c2) v = (i == j) ? (pad ? 1.f : v + lam) : v;
+      acc[t][r] = v;
+    }
+  });
+  float bcol[NB], z[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) bcol[c] = rc[c] * inv;
+  const bool ok = w1_solve_x<NB, false>(acc, bcol, lds, n, z);
+  if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
+  // x = Y_S^T z: z split into f16 hi + lo after a power-of-two scale
+  float zm = 0.f;
+#pragma unroll
+  for (int c = 0; c < NB; ++c) zm = fmaxf(zm, __builtin_fabsf(z[c]));
+  const int ez = split_exponent(wave_max(zm));
+  const float sz = ldexpf(1.f, ez);
+  half2v zh2[NB], zl2[NB];
+#pragma unroll
+  for (int c = 0; c < NB; ++c) {
+    const float t = z[c] * sz;
+    const _Float16 h = (_Float16)t;
+    const _Float16 l = (_Float16)(t - (float)h);
+    zh2[c] = half2v{h, h};
+    zl2[c] = half2v{l, l};
+  }
+  uint32_t w[NB][4][8];
+  dual_gather<NB>(w, cc, Ysp);
+  float px[4][8];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float a = 0.f;
+#pragma unroll
+      for (int c = 0; c < NB; ++c) {
+        const half2v hl = __builtin_bit_cast(half2v, w[c][s][t]);
+        a = __builtin_amdgcn_fdot2(hl, zh2[c], a, false);
+        a = __builtin_amdgcn_fdot2(hl, zl2[c], a, false);
+      }
+      px[s][t] = reduce_lanes16(a);
+    }
+  // lane (q, 0) holds dims 32s + 8q .. +7; (2^ey y)(2^ez z) -> x
+  const float un = ldexpf(1.f, -ey - ez);
+  if (m == 0) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int d = 32 * s + 8 * q + 4 * h;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = ok ? px[s][4 * h + e] * un : 0.f;
+        if (d < ld) *reinterpret_cast<float4*>(xrow + d) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+  }
+}
+
+// One wavefront per short light row (the tail of the LPT-ordered light list, every
+// row with <= kDualMaxRatings ratings), explicit, k in (64, 128], regParam > 0.
+__global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
+    float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
+    const uint32_t* __restrict__ Ysp, int32_t zero_row) {
+  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<4>::SIZE];
+  const int row = rows[blockIdx.x];
+  const int64_t pb = row_ptr[row];
+  const int n = (int)(row_ptr[row + 1] - pb);
+  const int ey = split_exponent(scal[0]);
+  float* xrow = X + (int64_t)row * ld;
+  if (n > kDualMaxRatings) {  // schedule contract broken: report the row, leave it zero
+    if ((threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
+    return;
+  }
+  if (n <= 32)
+    dual_row<2>(row, pb, n, col, val, Ysp, zero_row, ey, reg, xrow, ld, lds, status);
+  else
+    dual_row<4>(row, pb, n, col, val, Ysp, zero_row, ey, reg, xrow, ld, lds, status);
+}
+
 // Launch 2 (W1): heavy rows — fp64 sums of the fp32 chunk partials in a fixed
 // order (+ YtY in fp64 for implicit), one rounding, then the solve.  Entries are
 // reduced 16 at a time (a memory clobber keeps the groups' slot loops apart, so
@@ -2124,7 +2312,8 @@ size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src) {
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
-                   const int32_t* light_rows, int32_t n_light, const int32_t* heavy_rows,
+                   const int32_t* light_rows, int32_t n_light, int32_t n_light_primal,
+                   const int32_t* heavy_rows,
                    const int32_t* heavy_slot_begin, int32_t n_heavy, const int32_t* chunk_row,
                    const int64_t* chunk_begin, const int64_t* chunk_end, int32_t n_chunks,
                    const float* Y_src, int64_t n_src, float* X_dst, int32_t ld, int32_t k,
@@ -2136,6 +2325,11 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
               ld);
   ALS_REQUIRE(n_light >= 0 && n_heavy >= 0 && n_chunks >= 0, ALS_EINVAL,
               "als_solve_half: negative counts");
+  ALS_REQUIRE(n_light_primal >= 0 && n_light_primal <= n_light, ALS_EINVAL,
+              "als_solve_half: n_light_primal %d not in [0, n_light=%d]", n_light_primal, n_light);
+  ALS_REQUIRE(n_light_primal == n_light || (!implicit && k > 64 && reg > 0.f), ALS_EINVAL,
+              "als_solve_half: the dual path (light rows past n_light_primal) is for explicit "
+              "feedback at rank 65-128 with regParam > 0 only");
   ALS_REQUIRE(Y_src && X_dst && row_ptr && status_dev, ALS_EINVAL, "als_solve_half: null pointer");
   ALS_REQUIRE(!implicit || yty_packed, ALS_EINVAL, "als_solve_half: implicit needs yty_packed");
   ALS_REQUIRE(reg >= 0.f && alpha >= 0.f, ALS_EINVAL, "als_solve_half: reg/alpha must be >= 0");
@@ -2193,7 +2387,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       ALS_LAUNCH_CHECK();
     }
   }
-  const unsigned g1 = (phases & 1) ? (unsigned)(n_chunks + n_light) : 0u;
+  const unsigned g1 = (phases & 1) ? (unsigned)(n_chunks + n_light_primal) : 0u;
+  const unsigned gd = (phases & 1) ? (unsigned)(n_light - n_light_primal) : 0u;
   const unsigned g2 = (phases & 2) ? (unsigned)n_heavy : 0u;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
@@ -2218,10 +2413,15 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     float* slots_f = reinterpret_cast<float*>(slots);                                             \
     if (g1)                                                                                       \
       gram_solve_w1_kernel<IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,    \
-                                                   chunk_end, n_chunks, n_light, Y_src, X_dst,    \
-                                                   ld, k, reg, alpha, ytyC, slots_f, status_dev,  \
-                                                   scal, Ysp, kp, zero_row);                      \
+                                                   chunk_end, n_chunks, n_light_primal, Y_src,    \
+                                                   X_dst, ld, k, reg, alpha, ytyC, slots_f,       \
+                                                   status_dev, scal, Ysp, kp, zero_row);          \
     ALS_LAUNCH_CHECK();                                                                           \
+    if (gd) {                                                                                     \
+      gram_solve_dual_kernel<<<gd, 64, 0, st>>>(row_ptr, col, val, light_rows + n_light_primal,   \
+                                                X_dst, ld, reg, status_dev, scal, Ysp, zero_row); \
+      ALS_LAUNCH_CHECK();                                                                         \
+    }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot + 255) / 256, g2), 256, 0, st>>>(                 \
           heavy_slot_begin, slots_f, yty_packed);                                                 \

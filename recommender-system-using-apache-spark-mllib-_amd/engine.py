@@ -27,7 +27,8 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 
 DEFAULT_CHUNK = 2048  # ratings per heavy-row task
-MAX_RANK = 128       # k <= 64: one wavefront per system; 64 < k <= 128: one 4-wave workgroup
+MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
+DUAL_MAX_RATINGS = 64  # explicit, 64 < k <= 128: rows this short go through the n x n dual
 
 
 def ld_for(rank: int) -> int:
@@ -147,6 +148,7 @@ class RatingBlock:
     chunk_row: torch.Tensor
     chunk_begin: torch.Tensor
     chunk_end: torch.Tensor
+    n_short: int = 0  # light rows with <= DUAL_MAX_RATINGS ratings (the light list's tail)
 
 
 def build_block(row_ids: torch.Tensor, row_index: IdIndex, col_ids: torch.Tensor,
@@ -186,8 +188,12 @@ def schedule_block(n_rows, nnz, row_ptr, col, val, ws: Workspace, chunk: int = D
                                ptr(light), ptr(heavy), ptr(slot_begin), ptr(crow), ptr(cbeg),
                                ptr(cend), ptr(w), w.numel(), stream_ptr(dev)),
           "als_schedule_build")
+    n_short = 0
+    if n_light > 0:  # light rows are ordered by decreasing degree: the short ones are last
+        lr = light[:n_light].long()
+        n_short = int(((row_ptr[lr + 1] - row_ptr[lr]) <= DUAL_MAX_RATINGS).sum())
     return RatingBlock(n_rows, nnz, row_ptr, col, val, chunk, n_light, n_heavy, n_chunks, light,
-                       heavy, slot_begin, crow, cbeg, cend)
+                       heavy, slot_begin, crow, cbeg, cend, n_short)
 
 
 # ---------------------------------------------------------------------------
@@ -211,12 +217,17 @@ def compute_yty(Y: torch.Tensor, n: int, rank: int, ws: Workspace) -> torch.Tens
 def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, reg: float,
                implicit: bool, alpha: float, yty: Optional[torch.Tensor],
                status: torch.Tensor, ws: Workspace, phases: int = 15,
-               ws_chunks: Optional[int] = None) -> None:
+               ws_chunks: Optional[int] = None, dual: bool = True) -> None:
     """One computeFactors pass: X[row] <- solve(A_row, b_row) for every row of `block`.
     phases (bits, see als_hip.h): 4 = Y prep (max |Y|, split table), 8 = rating scale,
     1 = launch 1, 2 = launch 2; 15 = all in order.  ws_chunks: size the workspace for
-    this many heavy-row chunks (>= block.n_chunks; blocks sharing one Y prep)."""
+    this many heavy-row chunks (>= block.n_chunks; blocks sharing one Y prep).
+    dual: explicit, 64 < rank <= 128, reg > 0 — rows with <= DUAL_MAX_RATINGS ratings
+    are solved through the equivalent n x n dual system (als_hip.h n_light_primal);
+    False keeps every row on the k x k normal equations."""
     L = _lib.lib()
+    use_dual = dual and not implicit and rank > 64 and reg > 0
+    n_primal = block.n_light - block.n_short if use_dual else block.n_light
     w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0]),
                keep_scale=True)
     key = (w.data_ptr(), w.numel())
@@ -225,7 +236,8 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
         if phases == 0:
             return
     check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
-                           ptr(block.light_rows), block.n_light, ptr(block.heavy_rows),
+                           ptr(block.light_rows), block.n_light, n_primal,
+                           ptr(block.heavy_rows),
                            ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),
                            ptr(block.chunk_begin), ptr(block.chunk_end), block.n_chunks,
                            ptr(Y), Y.shape[0], ptr(X), X.shape[1], rank, float(reg),

@@ -19,7 +19,7 @@ import torch
 
 import als_mi355x.engine as E
 from oracle import als_oracle as O
-from helpers import planted, rel_row_err, report
+from helpers import planted, rel_row_err, rel_row_errs, report
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -236,6 +236,64 @@ def test_half_sweep_mixed_row_norms(outlier, implicit, rank):
     ev = rel_row_err(core.V[:, :rank].cpu().numpy(), V_ref)
     report(f"half_sweep_mixed_norms[x{outlier:g},rank={rank},implicit={implicit}]", ev)
     assert ev <= 1e-4
+
+
+def _degree_data(degrees, n_items, seed):
+    """Users with exactly the given degrees (distinct items each) plus one user rating
+    every item (so every item is rated); planted half-star ratings."""
+    rng = np.random.default_rng(seed)
+    us = [np.full(d, uid) for uid, d in enumerate(degrees)]
+    its = [rng.choice(n_items, d, replace=False) for d in degrees]
+    us.append(np.full(n_items, len(degrees)))
+    its.append(np.arange(n_items))
+    u = np.concatenate(us).astype(np.int32)
+    i = np.concatenate(its).astype(np.int32)
+    uf = rng.normal(0, 0.35, (len(degrees) + 1, 8))
+    vf = rng.normal(0, 0.35, (n_items, 8))
+    r = np.clip(np.round((3.6 + (uf[u] * vf[i]).sum(1) + rng.normal(0, 0.8, len(u))) * 2) / 2,
+                0.5, 5).astype(np.float32)
+    return u, i, r
+
+
+DUAL_DEGREES = [1, 2, 7, 15, 16, 17, 31, 32, 33, 40, 48, 63, 64, 65, 66, 90, 128, 129]
+
+
+@pytest.mark.parametrize("rank", [65, 96, 100, 128])
+def test_dual_short_rows_match_primal_and_oracle(rank):
+    """Explicit rows with <= 64 ratings at rank 65-128 go through the n x n dual
+    system (NB = 2 for n <= 32, 4 for n <= 64); the rest through the k x k primal.
+    Both forms vs the fp64 oracle of Spark's k x k normal equations, per row, with
+    the degrees around every class boundary (1, 16/17, 32/33, 64/65)."""
+    degrees = DUAL_DEGREES * 15
+    u, i, r = _degree_data(degrees, 400, seed=rank)
+    core = _core(u, i, r, chunk=256)
+    ub = core.user_block
+    assert ub.n_short == sum(d <= E.DUAL_MAX_RATINGS for d in degrees)
+    core.init_factors(rank, seed=3)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(rank)
+    V0 = torch.randn((core.n_items, rank), generator=g, device=DEV)
+    V0 = V0 / torch.linalg.vector_norm(V0, dim=1, keepdim=True)
+    core.V[:, :rank] = V0
+    V0 = V0.cpu().numpy()
+    U_ref = O.half_sweep(ub.row_ptr.cpu().numpy(), ub.col.cpu().numpy(), ub.val.cpu().numpy(),
+                         V0, 0.1)
+    deg = np.diff(ub.row_ptr.cpu().numpy())
+    out = {}
+    for dual in (True, False):
+        core.U.fill_(7.0)  # every written entry must be overwritten (pad columns with 0)
+        core.status.zero_()
+        E.solve_half(ub, core.V, core.U, rank, 0.1, False, 1.0, None, core.status, core.ws,
+                     dual=dual)
+        torch.cuda.synchronize()
+        core.check_status()
+        U = core.U.cpu().numpy()
+        assert np.all(U[:, rank:] == 0.0)
+        e = rel_row_errs(U[:, :rank], U_ref)
+        out[dual] = {f"deg<={b}": float(e[(deg <= b) & (deg > a)].max())
+                     for a, b in ((0, 16), (16, 32), (32, 64), (64, 10 ** 9))}
+        assert e.max() <= 1e-4, (dual, out[dual])
+    report(f"dual_vs_primal[rank={rank}]", out)
 
 
 def test_failed_pivot_raises_with_row():

@@ -10,20 +10,37 @@ SURVEY §3A.5), so resuming from U at iteration t and running to T gives the sam
 factors as an uninterrupted T-iteration fit.
 
 Layout of a checkpoint directory (host formats, nothing pickled):
-    als_state.json      {"format": 1, "iteration": t, "rank", "regParam",
-                         "implicitPrefs", "alpha", "data": fingerprint}
-    user_ids.npy        int32 [n_users]   dense order (ascending ids)
-    user_factors.npy    float32 [n_users, rank]
-    item_ids.npy, item_factors.npy        the same for V (needed only when the
-                        checkpoint is already at the requested iteration count:
-                        V_t came from U_{t-1}, which is not kept)
-Files are written to temporaries and renamed, the JSON last, so a job killed
-mid-write leaves the previous checkpoint intact.
+    als_state.json      {"format": 2, "iteration": t, "generation": "gen-<t>-<tag>",
+                         "rank", "regParam", "implicitPrefs", "alpha",
+                         "init": {"seed": s} | {"U0": sha1}, "data": fingerprint}
+    gen-<t>-<tag>/      one complete generation:
+        user_ids.npy        int32 [n_users]   dense order (ascending ids)
+        user_factors.npy    float32 [n_users, rank]
+        item_ids.npy, item_factors.npy        the same for V (needed only when the
+                            checkpoint is already at the requested iteration count:
+                            V_t came from U_{t-1}, which is not kept)
+A save writes a NEW generation directory (fsynced), then atomically replaces
+als_state.json (the commit point), then deletes the older generations.  A job
+killed at any point leaves als_state.json naming one complete generation, and
+its factors are always those of the iteration the JSON states.
+
+Matching: the ratings fingerprint, rank, regParam, implicitPrefs and alpha must
+agree.  In "auto" mode (ALS.fit with a checkpoint dir, Spark's checkpointInterval
+semantics: a checkpoint never changes the model) the initialisation must agree
+too — a different seed or explicit start is a different fit; resume=True is the
+explicit "continue from this checkpoint" and ignores the initialisation.
+
+Multi-process: resume_point_agreed() lets process 0 decide and broadcasts the
+decision (and the factors) to every rank, so all ranks start at the same
+iteration from the same state even without a shared filesystem.
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
+import shutil
+import uuid
 from dataclasses import dataclass
 from typing import Optional
 
@@ -34,7 +51,8 @@ IDS = "user_ids.npy"
 FACTORS = "user_factors.npy"
 IIDS = "item_ids.npy"
 IFACTORS = "item_factors.npy"
-FORMAT = 1
+FORMAT = 2
+_GEN = "gen-"
 
 
 @dataclass
@@ -49,33 +67,72 @@ class State:
     U: np.ndarray
     item_ids: np.ndarray
     V: np.ndarray
+    init: Optional[dict] = None
 
 
-def _replace_npy(path: str, arr: np.ndarray) -> None:
-    tmp = path + ".tmp.npy"
-    np.save(tmp, arr, allow_pickle=False)
-    os.replace(tmp, path)
+def init_key(seed, U0) -> dict:
+    """How a fit starts: its seed, or a digest of an explicit initial U."""
+    if U0 is not None:
+        a = np.ascontiguousarray(np.asarray(
+            U0.detach().cpu().numpy() if hasattr(U0, "detach") else U0, dtype=np.float32))
+        return {"U0": hashlib.sha1(a.tobytes()).hexdigest() + f":{a.shape}"}
+    return {"seed": int(seed)}
+
+
+def _fsync_file(path: str) -> None:
+    with open(path, "rb") as f:
+        os.fsync(f.fileno())
+
+
+def _fsync_dir(path: str) -> None:
+    try:
+        fd = os.open(path, os.O_RDONLY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    except OSError:
+        pass
+    finally:
+        os.close(fd)
 
 
 def save(dirpath: str, iteration: int, rank: int, reg: float, implicit: bool, alpha: float,
-         data: dict, user_ids, U, item_ids, V) -> None:
-    """Write the state after `iteration` completed iterations."""
+         data: dict, user_ids, U, item_ids, V, init: Optional[dict] = None) -> None:
+    """Write the state after `iteration` completed iterations (a new generation, then
+    the atomic commit of als_state.json, then removal of the older generations)."""
     os.makedirs(dirpath, exist_ok=True)
+    gen = f"{_GEN}{int(iteration):06d}-{uuid.uuid4().hex[:8]}"
+    tmp = os.path.join(dirpath, "." + gen + ".tmp")
+    os.makedirs(tmp)
     for ids_name, f_name, ids, F in ((IDS, FACTORS, user_ids, U), (IIDS, IFACTORS, item_ids, V)):
         ids = np.ascontiguousarray(np.asarray(ids), dtype=np.int32)
         F = np.ascontiguousarray(np.asarray(F), dtype=np.float32)
         if F.shape != (ids.shape[0], rank):
+            shutil.rmtree(tmp, ignore_errors=True)
             raise ValueError(f"factor table {F.shape} does not match {ids.shape[0]} ids x rank "
                              f"{rank}")
-        _replace_npy(os.path.join(dirpath, ids_name), ids)
-        _replace_npy(os.path.join(dirpath, f_name), F)
-    meta = {"format": FORMAT, "iteration": int(iteration), "rank": int(rank),
+        for name, arr in ((ids_name, ids), (f_name, F)):
+            p = os.path.join(tmp, name)
+            np.save(p, arr, allow_pickle=False)
+            _fsync_file(p)
+    _fsync_dir(tmp)
+    os.replace(tmp, os.path.join(dirpath, gen))
+    _fsync_dir(dirpath)
+    meta = {"format": FORMAT, "iteration": int(iteration), "generation": gen, "rank": int(rank),
             "regParam": float(reg), "implicitPrefs": bool(implicit), "alpha": float(alpha),
-            "data": data}
-    tmp = os.path.join(dirpath, STATE + ".tmp")
-    with open(tmp, "w") as f:
+            "init": init, "data": data}
+    tmpj = os.path.join(dirpath, STATE + ".tmp")
+    with open(tmpj, "w") as f:
         json.dump(meta, f)
-    os.replace(tmp, os.path.join(dirpath, STATE))
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmpj, os.path.join(dirpath, STATE))  # the commit point
+    _fsync_dir(dirpath)
+    for name in os.listdir(dirpath):  # older generations, stale temporaries
+        if name != gen and (name.startswith(_GEN) or (name.startswith("." + _GEN)
+                                                       and name.endswith(".tmp"))):
+            shutil.rmtree(os.path.join(dirpath, name), ignore_errors=True)
 
 
 def load(dirpath: str) -> Optional[State]:
@@ -85,17 +142,24 @@ def load(dirpath: str) -> Optional[State]:
         return None
     with open(p) as f:
         m = json.load(f)
-    if m.get("format") != FORMAT:
-        raise ValueError(f"{p}: unknown checkpoint format {m.get('format')}")
-    arr = [np.load(os.path.join(dirpath, n), allow_pickle=False)
+    fmt = m.get("format")
+    if fmt == 2:
+        base = os.path.join(dirpath, m["generation"])
+    elif fmt == 1:  # round-2 layout: files next to the JSON
+        base = dirpath
+    else:
+        raise ValueError(f"{p}: unknown checkpoint format {fmt}")
+    arr = [np.load(os.path.join(base, n), allow_pickle=False)
            for n in (IDS, FACTORS, IIDS, IFACTORS)]
     return State(int(m["iteration"]), int(m["rank"]), float(m["regParam"]),
-                 bool(m["implicitPrefs"]), float(m["alpha"]), m["data"], *arr)
+                 bool(m["implicitPrefs"]), float(m["alpha"]), m["data"], *arr,
+                 init=m.get("init"))
 
 
 def mismatch(st: State, rank: int, reg: float, implicit: bool, alpha: float, data: dict,
-             user_ids) -> Optional[str]:
-    """Why `st` cannot seed this fit (None when it can)."""
+             user_ids, init: Optional[dict] = None) -> Optional[str]:
+    """Why `st` cannot seed this fit (None when it can).  init: compare the
+    initialisation too (auto mode)."""
     if st.rank != rank:
         return f"rank {st.rank} != {rank}"
     if st.reg != float(reg) or st.implicit != bool(implicit) or \
@@ -108,15 +172,20 @@ def mismatch(st: State, rank: int, reg: float, implicit: bool, alpha: float, dat
         return "user ids differ"
     if st.U.shape != (ids.shape[0], rank):
         return f"factor table shape {st.U.shape}"
+    if init is not None and st.init != init:
+        return f"initialisation differs (checkpoint {st.init}, now {init})"
     return None
 
 
 def resume_point(dirpath: Optional[str], resume, engine, rank: int, reg: float, implicit: bool,
-                 alpha: float, max_iter: int):
+                 alpha: float, max_iter: int, init: Optional[dict] = None,
+                 fingerprint: Optional[dict] = None):
     """(start iteration, U0, V0) for engine.fit; U0/V0 None for a fresh start, V0 set
     only when the checkpoint is already at max_iter.  resume: False = start fresh;
-    True = the checkpoint must exist and match (ValueError otherwise); "auto" = use
-    it when it matches, else start fresh."""
+    True = the checkpoint must exist and match (ValueError otherwise; the
+    initialisation is not compared); "auto" = use it when it matches, initialisation
+    included, else start fresh.  fingerprint: the engine's (precomputed by every
+    rank of a sharded engine, where it is a collective)."""
     if not resume or not dirpath:
         return 0, None, None
     st = load(dirpath)
@@ -125,7 +194,9 @@ def resume_point(dirpath: Optional[str], resume, engine, rank: int, reg: float, 
             raise ValueError(f"no ALS checkpoint in {dirpath}")
         return 0, None, None
     ids = engine.user_factor_ids().cpu().numpy()
-    why = mismatch(st, rank, reg, implicit, alpha, engine.fingerprint(), ids)
+    fp = fingerprint if fingerprint is not None else engine.fingerprint()
+    why = mismatch(st, rank, reg, implicit, alpha, fp, ids,
+                   init=None if resume is True else init)
     if why is None and st.iteration > max_iter:
         why = f"checkpoint is at iteration {st.iteration} > maxIter {max_iter}"
     if why is not None:
@@ -135,16 +206,60 @@ def resume_point(dirpath: Optional[str], resume, engine, rank: int, reg: float, 
     return st.iteration, st.U, (st.V if st.iteration == max_iter else None)
 
 
+def resume_point_agreed(dirpath: Optional[str], resume, engine, rank: int, reg: float,
+                        implicit: bool, alpha: float, max_iter: int, init: Optional[dict],
+                        group, device):
+    """resume_point for the ranks of a process group: every rank computes the
+    fingerprint (a collective), process 0 alone reads the checkpoint and decides, and
+    the decision — start iteration, error — and the factors are broadcast, so every
+    rank starts at the same iteration from the same state (or every rank raises)."""
+    import torch
+    import torch.distributed as dist
+    if not resume or not dirpath:
+        return 0, None, None
+    fp = engine.fingerprint()  # collective: every rank
+    proc = dist.get_rank(group)
+    start, U, V, err = 0, None, None, None
+    if proc == 0:
+        try:
+            start, U, V = resume_point(dirpath, resume, engine, rank, reg, implicit, alpha,
+                                       max_iter, init, fingerprint=fp)
+        except ValueError as e:
+            err = str(e)
+    head = [start, V is not None, err]
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast_object_list(head, src=src, group=group)
+    start, has_v, err = head
+    if err is not None:
+        raise ValueError(err)
+    if start == 0 and not has_v:
+        return 0, None, None
+
+    def bcast(F, n):
+        t = (torch.as_tensor(F).to(device, torch.float32).contiguous() if proc == 0 else
+             torch.empty((n, rank), dtype=torch.float32, device=device))
+        dist.broadcast(t, src=src, group=group)
+        return t
+
+    U = bcast(U, engine.n_users)
+    V = bcast(V, engine.n_items) if has_v else None
+    return start, U, V
+
+
 def maybe_save(dirpath: Optional[str], interval: int, it_done: int, engine, rank: int,
-               reg: float, implicit: bool, alpha: float, writer: bool = True) -> None:
+               reg: float, implicit: bool, alpha: float, writer: bool = True,
+               init: Optional[dict] = None) -> None:
     """After iteration `it_done` (1-based count): write when it is a multiple of
-    `interval` (Spark's checkpointInterval; <= 0 disables)."""
+    `interval` (Spark's checkpointInterval; <= 0 disables).  check_status() and
+    fingerprint() run on every rank (collectives of a sharded engine); only the
+    writer fetches the factors to the host (without caching dense copies)."""
     if not dirpath or interval is None or interval <= 0 or it_done % interval != 0:
         return
     engine.check_status()  # never checkpoint the state of a failed solve
-    uids, U = engine.user_factors()
-    iids, V = engine.item_factors()
     data = engine.fingerprint()
-    if writer:
-        save(dirpath, it_done, rank, reg, implicit, alpha, data, uids.cpu().numpy(),
-             U.float().cpu().numpy(), iids.cpu().numpy(), V.float().cpu().numpy())
+    if not writer:
+        return
+    uids, U = engine.user_factors(cache=False)
+    iids, V = engine.item_factors(cache=False)
+    save(dirpath, it_done, rank, reg, implicit, alpha, data, uids.cpu().numpy(),
+         U.float().cpu().numpy(), iids.cpu().numpy(), V.float().cpu().numpy(), init=init)

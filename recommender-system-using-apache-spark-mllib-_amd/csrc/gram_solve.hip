@@ -1910,7 +1910,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
 
 // ---------------------------------------------------------------------------
 // Short explicit rows at 64 < k <= 128: the n x n dual system.
-// For a row with n <= 64 ratings r_j on the factor rows y_j (Y_S = n x k):
+// For a row with n <= 96 ratings r_j on the factor rows y_j (Y_S = n x k):
 //   x = (Y_S^T Y_S + lambda n I)^-1 Y_S^T r  =  Y_S^T (Y_S Y_S^T + lambda n I)^-1 r
 // (push-through identity (Y^T Y + c I) Y^T = Y^T (Y Y^T + c I); both systems are
 // SPD for lambda n > 0).  So x is the solution of Spark's CholeskySolver on the
@@ -1921,79 +1921,90 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
 // permutation of the primal kernels — so w1_solve_x consumes the Gram tiles as
 // the MFMAs leave them and pads ratings j >= n the way it pads dims.
 //  * Gram G = 2^2ey Y_S Y_S^T on v_mfma_f32_16x16x32_f16 from the split table
-//    (hi | lo words of 2^ey Y): MFMA K = dims, 4 k-steps of 32; operand (c, s) on
-//    lane (q, m) = dims 32s + 8q .. +7 of rating m * NB + c; hi.hi + hi.lo + lo.hi
-//    per tile per k-step (fp32-grade products, as the primal Gram).
+//    (hi | lo words of 2^ey Y): MFMA K = dims, 4 k-steps of 32 dims, streamed
+//    (step s+1's gathers in flight during step s's MFMAs); operand (c, s) on lane
+//    (q, m) = dims 32s + 8q .. +7 of rating m * NB + c; hi.hi + hi.lo + lo.hi per
+//    tile per k-step (fp32-grade products, as the primal Gram).
 //  * solve: w1_solve_x<NB> (fp32 MFMA tile products), z_j on the lanes of block c.
 //  * x = Y_S^T z from the same rows re-gathered (L2-hot): a split word is the f16
 //    pair (hi, lo) of one entry, so v_dot2_f32_f16 against (z_hi, z_hi) and
 //    (z_lo, z_lo) (z split after a power-of-two scale) accumulates (hi + lo) z in
 //    fp32; summed over the 16 lanes of a row group.
-// NB = 2 for n <= 32, 4 for n <= 64: a wave-uniform branch of one kernel.
-constexpr int kDualMaxRatings = 64;
+// NB = 2 (n <= 32), 4 (n <= 64), 6 (n <= 96): a wave-uniform branch of one kernel.
+constexpr int kDualMaxRatings = 96;
 
+// The 8 split words of dims 32s + 8q .. +7 of each operand block's rating.
 template <int NB>
-__device__ __forceinline__ void dual_gather(uint32_t (&w)[NB][4][8], const int (&cc)[NB],
-                                            const uint32_t* __restrict__ Ysp) {
+__device__ __forceinline__ void dual_gather_step(uint32_t (&w)[NB][8], const int (&cc)[NB], int s,
+                                                 const uint32_t* __restrict__ Ysp) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
-  for (int c = 0; c < NB; ++c)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const uint32_t* p = Ysp + (uint64_t)(uint32_t)cc[c] * 128u + 32 * s + 8 * q;
-      const uint4 a = *reinterpret_cast<const uint4*>(p);
-      const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
-      w[c][s][0] = a.x; w[c][s][1] = a.y; w[c][s][2] = a.z; w[c][s][3] = a.w;
-      w[c][s][4] = b.x; w[c][s][5] = b.y; w[c][s][6] = b.z; w[c][s][7] = b.w;
-    }
+  for (int c = 0; c < NB; ++c) {
+    const uint32_t* p = Ysp + (uint64_t)(uint32_t)cc[c] * 128u + 32 * s + 8 * q;
+    const uint4 a = *reinterpret_cast<const uint4*>(p);
+    const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
+    w[c][0] = a.x; w[c][1] = a.y; w[c][2] = a.z; w[c][3] = a.w;
+    w[c][4] = b.x; w[c][5] = b.y; w[c][6] = b.z; w[c][7] = b.w;
+  }
 }
 
 template <int NB>
-__device__ __forceinline__ void dual_row(int row, int64_t pb, int n,
-                                         const int32_t* __restrict__ col,
-                                         const float* __restrict__ val,
-                                         const uint32_t* __restrict__ Ysp, int zero_row, int ey,
-                                         float reg, float* __restrict__ xrow, int ld,
+__device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
+                                         const float (&rj)[2], const uint32_t* __restrict__ Ysp,
+                                         int ey, float reg, float* __restrict__ xrow, int ld,
                                          float* __restrict__ lds, int32_t* __restrict__ status) {
   constexpr int NT = NB * (NB + 1) / 2;
   typedef FullTiles<NB> TS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  // lane j < n loads rating j; operand block c of lane (q, m) is rating m * NB + c
-  const int cj = lane < n ? col[pb + lane] : zero_row;
-  const float rj = lane < n ? val[pb + lane] : 0.f;
+  // operand block c of lane (q, m) is rating j = m * NB + c (held by lane j % 64 in
+  // register j / 64 of the staging pair)
   int cc[NB];
   float rc[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
-    cc[c] = __shfl(cj, m * NB + c);
-    rc[c] = __shfl(rj, m * NB + c);
+    const int j = m * NB + c;
+    const int c0 = __shfl(cj[0], j & 63);
+    const float r0 = __shfl(rj[0], j & 63);
+    if constexpr (NB * 16 > 64) {
+      const int c1 = __shfl(cj[1], j & 63);
+      const float r1 = __shfl(rj[1], j & 63);
+      cc[c] = j < 64 ? c0 : c1;
+      rc[c] = j < 64 ? r0 : r1;
+    } else {
+      cc[c] = c0;
+      rc[c] = r0;
+    }
   }
   floatx4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  {
-    uint32_t w[NB][4][8];
-    dual_gather<NB>(w, cc, Ysp);
-    static_for<4>([&](auto sc) {
-      constexpr int s = decltype(sc)::value;
-      uint32_t hi[NB][4], lo[NB][4];
+  // NB <= 4: step s+1's gathers in flight during step s; NB = 6: one step of
+  // registers (the two waves per SIMD overlap each other's gathers instead)
+  constexpr int NBUF = NB <= 4 ? 2 : 1;
+  uint32_t w[NBUF][NB][8];
+  dual_gather_step<NB>(w[0], cc, 0, Ysp);
+  static_for<4>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    constexpr int cur = s % NBUF;
+    if constexpr (NBUF == 2 && s + 1 < 4) dual_gather_step<NB>(w[(s + 1) % NBUF], cc, s + 1, Ysp);
+    if constexpr (NBUF == 1 && s > 0) dual_gather_step<NB>(w[0], cc, s, Ysp);
+    uint32_t hi[NB][4], lo[NB][4];
 #pragma unroll
-      for (int c = 0; c < NB; ++c)
+    for (int c = 0; c < NB; ++c)
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          hi[c][p] = __builtin_amdgcn_perm(w[c][s][2 * p + 1], w[c][s][2 * p], 0x05040100u);
-          lo[c][p] = __builtin_amdgcn_perm(w[c][s][2 * p + 1], w[c][s][2 * p], 0x07060302u);
-        }
-      static_for<NT>([&](auto ti) {
-        constexpr int t = decltype(ti)::value;
-        constexpr int a = TS::l1(t), b = TS::l2(t);
-        const half8v ha = as_h8(hi[a]), hb = as_h8(hi[b]);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, as_h8(lo[b]), acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(lo[a]), hb, acc[t], 0, 0, 0);
-      });
+      for (int p = 0; p < 4; ++p) {
+        hi[c][p] = __builtin_amdgcn_perm(w[cur][c][2 * p + 1], w[cur][c][2 * p], 0x05040100u);
+        lo[c][p] = __builtin_amdgcn_perm(w[cur][c][2 * p + 1], w[cur][c][2 * p], 0x07060302u);
+      }
+    static_for<NT>([&](auto ti) {
+      constexpr int t = decltype(ti)::value;
+      constexpr int a = TS::l1(t), b = TS::l2(t);
+      const half8v ha = as_h8(hi[a]), hb = as_h8(hi[b]);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, hb, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ha, as_h8(lo[b]), acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(lo[a]), hb, acc[t], 0, 0, 0);
     });
-  }
+  });
   // (2^2ey G + 2^2ey lambda n I) z = 2^2ey r; ratings j >= n: identity rows, rhs 0
   const float inv = ldexpf(1.f, 2 * ey);
   const float lam = (float)((double)reg * (double)n) * inv;
@@ -2030,22 +2041,25 @@ __device__ __forceinline__ void dual_row(int row, int64_t pb, int n,
     zh2[c] = half2v{h, h};
     zl2[c] = half2v{l, l};
   }
-  uint32_t w[NB][4][8];
-  dual_gather<NB>(w, cc, Ysp);
   float px[4][8];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
+  dual_gather_step<NB>(w[0], cc, 0, Ysp);
+  static_for<4>([&](auto sc) {
+    constexpr int s = decltype(sc)::value;
+    constexpr int cur = s % NBUF;
+    if constexpr (NBUF == 2 && s + 1 < 4) dual_gather_step<NB>(w[(s + 1) % NBUF], cc, s + 1, Ysp);
+    if constexpr (NBUF == 1 && s > 0) dual_gather_step<NB>(w[0], cc, s, Ysp);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float a = 0.f;
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
-        const half2v hl = __builtin_bit_cast(half2v, w[c][s][t]);
+        const half2v hl = __builtin_bit_cast(half2v, w[cur][c][t]);
         a = __builtin_amdgcn_fdot2(hl, zh2[c], a, false);
         a = __builtin_amdgcn_fdot2(hl, zl2[c], a, false);
       }
       px[s][t] = reduce_lanes16(a);
     }
+  });
   // lane (q, 0) holds dims 32s + 8q .. +7; (2^ey y)(2^ez z) -> x
   const float un = ldexpf(1.f, -ey - ez);
   if (m == 0) {
@@ -2062,27 +2076,39 @@ __device__ __forceinline__ void dual_row(int row, int64_t pb, int n,
   }
 }
 
-// One wavefront per short light row (the tail of the LPT-ordered light list, every
+// One wavefront per short light row (the tail of the longest-first light list: every
 // row with <= kDualMaxRatings ratings), explicit, k in (64, 128], regParam > 0.
 __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
     float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
     const uint32_t* __restrict__ Ysp, int32_t zero_row) {
-  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<4>::SIZE];
+  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<6>::SIZE];
+  const int lane = threadIdx.x & 63;
   const int row = rows[blockIdx.x];
   const int64_t pb = row_ptr[row];
   const int n = (int)(row_ptr[row + 1] - pb);
   const int ey = split_exponent(scal[0]);
   float* xrow = X + (int64_t)row * ld;
   if (n > kDualMaxRatings) {  // schedule contract broken: report the row, leave it zero
-    if ((threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
+    if (lane == 0) atomicCAS(status, 0, row + 1);
     return;
   }
+  // ratings j = lane and j = lane + 64 (missing ones point at the zero row)
+  int cj[2];
+  float rj[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int j = lane + 64 * h;
+    cj[h] = j < n ? col[pb + j] : zero_row;
+    rj[h] = j < n ? val[pb + j] : 0.f;
+  }
   if (n <= 32)
-    dual_row<2>(row, pb, n, col, val, Ysp, zero_row, ey, reg, xrow, ld, lds, status);
+    dual_row<2>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+  else if (n <= 64)
+    dual_row<4>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
   else
-    dual_row<4>(row, pb, n, col, val, Ysp, zero_row, ey, reg, xrow, ld, lds, status);
+    dual_row<6>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
 }
 
 // Launch 2 (W1): heavy rows — fp64 sums of the fp32 chunk partials in a fixed

@@ -412,8 +412,10 @@ class ShardedALS:
         """ALSCore.fit's contract.  Checkpoints hold the dense global factors (written
         by process 0, read by every rank), so a job may resume on another world size."""
         from . import checkpoint as C
-        start, Uc, Vc = C.resume_point(checkpoint_dir, resume, self, rank, reg, implicit, alpha,
-                                       max_iter)
+        init = C.init_key(seed, U0 if U0 is not None else U0_global) if checkpoint_dir else None
+        # process 0 decides and broadcasts (start, factors): every rank resumes alike
+        start, Uc, Vc = C.resume_point_agreed(checkpoint_dir, resume, self, rank, reg, implicit,
+                                              alpha, max_iter, init, self.group, self.device)
         if Uc is not None:
             U0, U0_global = None, Uc
         self.init_factors(rank, seed, U0, U0_global)
@@ -423,7 +425,7 @@ class ShardedALS:
         for it in range(start, max_iter):
             self.iterate(reg, implicit, alpha)
             C.maybe_save(checkpoint_dir, checkpoint_interval, it + 1, self, rank, reg, implicit,
-                         alpha, writer=self.proc == 0)
+                         alpha, writer=self.proc == 0, init=init)
         if checkpoint_dir:
             dist.barrier(group=self.group)
         self.check_status()
@@ -454,13 +456,17 @@ class ShardedALS:
         return self.users.ids()
 
     # ---- serving protocol (engine.ALSCore's), on the replicated factors ----
-    def _dense(self, user_side: bool) -> torch.Tensor:
-        """Dense-order copy [n, ld] of one replicated factor table (cached per fit state)."""
-        if user_side not in self._dense_cache:
-            side, full = (self.users, self.U_full) if user_side else (self.items, self.V_full)
-            dense = torch.arange(side.n, device=full.device)
-            self._dense_cache[user_side] = full[side.padded(dense).long()].contiguous()
-        return self._dense_cache[user_side]
+    def _dense(self, user_side: bool, cache: bool = True) -> torch.Tensor:
+        """Dense-order copy [n, ld] of one replicated factor table (cached per fit state
+        unless cache=False)."""
+        if user_side in self._dense_cache:
+            return self._dense_cache[user_side]
+        side, full = (self.users, self.U_full) if user_side else (self.items, self.V_full)
+        dense = torch.arange(side.n, device=full.device)
+        t = full[side.padded(dense).long()].contiguous()
+        if cache:
+            self._dense_cache[user_side] = t
+        return t
 
     def _ids(self, x) -> torch.Tensor:
         return torch.as_tensor(x).to(self.device).to(torch.int32)
@@ -500,7 +506,7 @@ class ShardedALS:
                 continue
             idx, sc = self.K.topk(loc[c], b - a, Vd, other.n, self.rank, top)
             keys.append(side.ids()[a:b])
-            ids.append(oids[idx[:, :t].long()])
+            ids.append(oids[idx[:, :t].long().clamp(min=0)])  # empty slots: score -inf
             scs.append(sc[:, :t])
         if not keys:
             e = torch.empty((0, t), device=self.device)
@@ -523,7 +529,7 @@ class ShardedALS:
         Q = self._dense(user_side).index_select(0, rows).contiguous()
         idx, sc = self.K.topk(Q, keys.numel(), self._dense(not user_side), other.n, self.rank,
                               top)
-        return keys, other.ids()[idx[:, :t].long()], sc[:, :t]
+        return keys, other.ids()[idx[:, :t].long().clamp(min=0)], sc[:, :t]
 
     def recommend_users(self, top: int):
         _, ids, sc = self.recommend_all(top, True)
@@ -534,8 +540,8 @@ class ShardedALS:
         return ids, sc
 
     # ---- factor views in dense order (replicated on every rank) ----
-    def user_factors(self):
-        return self.users.ids(), self._dense(True)[:, :self.rank]
+    def user_factors(self, cache: bool = True):
+        return self.users.ids(), self._dense(True, cache)[:, :self.rank]
 
-    def item_factors(self):
-        return self.items.ids(), self._dense(False)[:, :self.rank]
+    def item_factors(self, cache: bool = True):
+        return self.items.ids(), self._dense(False, cache)[:, :self.rank]

@@ -28,7 +28,7 @@ from ._lib import check, ptr, stream_ptr
 
 DEFAULT_CHUNK = 2048  # ratings per heavy-row task
 MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
-DUAL_MAX_RATINGS = 64  # explicit, 64 < k <= 128: rows this short go through the n x n dual
+DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
 
 
 def ld_for(rank: int) -> int:
@@ -275,6 +275,13 @@ def rmse_pairs(u, i, r, uidx: IdIndex, iidx: IdIndex, U, V, rank: int, ws: Works
     return out
 
 
+def ids_of(ids: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """Ids of top-k dense rows.  A slot the kernel left empty (idx -1, score -inf: every
+    score of that query row NaN, from non-finite factors) keeps a placeholder id; the
+    callers drop slots whose score is not finite (valid_slots)."""
+    return ids[idx.long().clamp(min=0)]
+
+
 def topk_rows(Q: torch.Tensor, n_q: int, V: torch.Tensor, n_v: int, rank: int, top: int):
     """(idx int32 [n_q, top], score f32 [n_q, top]); idx = dense V row, -1 past n_v."""
     L = _lib.lib()
@@ -430,8 +437,9 @@ class ALSCore:
         write U, V every checkpoint_interval iterations (checkpoint.py); resume
         (True / "auto"): continue from the checkpoint there at its iteration."""
         from . import checkpoint as C
+        init = C.init_key(seed, U0) if checkpoint_dir else None
         start, Uc, Vc = C.resume_point(checkpoint_dir, resume, self, rank, reg, implicit, alpha,
-                                       max_iter)
+                                       max_iter, init)
         self.init_factors(rank, seed, Uc if Uc is not None else U0)
         if Vc is not None:
             self.V[:, :rank] = _to_device(Vc, torch.float32, self.device)
@@ -439,7 +447,7 @@ class ALSCore:
         for it in range(start, max_iter):
             self.iterate(reg, implicit, alpha)
             C.maybe_save(checkpoint_dir, checkpoint_interval, it + 1, self, rank, reg, implicit,
-                         alpha)
+                         alpha, init=init)
         self.check_status()
         return self
 
@@ -483,7 +491,7 @@ class ALSCore:
         qi, Q, oi, Vo = self._sides(user_side)
         idx, sc = topk_rows(Q, qi.n, Vo, oi.n, self.rank, top)
         t = min(int(top), oi.n)
-        return qi.ids(), oi.ids()[idx[:, :t].long()], sc[:, :t]
+        return qi.ids(), ids_of(oi.ids(), idx[:, :t]), sc[:, :t]
 
     def recommend_subset(self, ids, top: int, user_side: bool = True):
         """recommendForUserSubset / ForItemSubset: distinct known ids of `ids`
@@ -500,7 +508,7 @@ class ALSCore:
                 torch.empty((0, t), dtype=torch.float32, device=self.device)
         Qs = Q.index_select(0, rows.long()).contiguous()
         idx, sc = topk_rows(Qs, keys.numel(), Vo, oi.n, self.rank, top)
-        return keys, oi.ids()[idx[:, :t].long()], sc[:, :t]
+        return keys, ids_of(oi.ids(), idx[:, :t]), sc[:, :t]
 
     def recommend_users(self, top: int):
         """For every user (dense order): top items as (item ids, scores)."""
@@ -511,8 +519,8 @@ class ALSCore:
         _, ids, sc = self.recommend_all(top, False)
         return ids, sc
 
-    def user_factors(self):
+    def user_factors(self, cache: bool = True):
         return self.uidx.ids(), self.U[:, :self.rank]
 
-    def item_factors(self):
+    def item_factors(self, cache: bool = True):
         return self.iidx.ids(), self.V[:, :self.rank]

@@ -248,7 +248,9 @@ class ALSModel:
         keys = keys.cpu().numpy()
         ids = ids.cpu().numpy()
         sc = sc.cpu().numpy()
-        recs = [[(int(a), float(b)) for a, b in zip(ri, rs)] for ri, rs in zip(ids, sc)]
+        # empty slots (score -inf: a query row whose every score is NaN) are dropped
+        recs = [[(int(a), float(b)) for a, b in zip(ri, rs) if np.isfinite(b)]
+                for ri, rs in zip(ids, sc)]
         return pd.DataFrame({key_col: keys, "recommendations": recs})
 
     def recommendForAllUsers(self, numItems: int):

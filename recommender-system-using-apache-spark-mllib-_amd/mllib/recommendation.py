@@ -116,7 +116,7 @@ class MatrixFactorizationModel:
             raise KeyError(f"unknown id {key}")
         ids, sc = ids.cpu().numpy()[0], sc.cpu().numpy()[0]
         return [Rating(key, int(a), float(s)) if user_side else Rating(int(a), key, float(s))
-                for a, s in zip(ids, sc)]
+                for a, s in zip(ids, sc) if np.isfinite(s)]
 
     def recommendProducts(self, user: int, num: int) -> List[Rating]:
         return self._one(int(user), num, True)
@@ -127,7 +127,8 @@ class MatrixFactorizationModel:
     def recommendProductsForUsers(self, num: int):
         keys, ids, sc = self._core.recommend_all(int(num), True)
         keys, ids, sc = keys.cpu().numpy(), ids.cpu().numpy(), sc.cpu().numpy()
-        return [(int(k), [Rating(int(k), int(a), float(s)) for a, s in zip(ri, rs)])
+        return [(int(k), [Rating(int(k), int(a), float(s)) for a, s in zip(ri, rs)
+                          if np.isfinite(s)])
                 for k, ri, rs in zip(keys, ids, sc)]
 
     def save(self, sc, path: str, overwrite: bool = False) -> None:
@@ -149,7 +150,8 @@ class MatrixFactorizationModel:
     def recommendUsersForProducts(self, num: int):
         keys, ids, sc = self._core.recommend_all(int(num), False)
         keys, ids, sc = keys.cpu().numpy(), ids.cpu().numpy(), sc.cpu().numpy()
-        return [(int(k), [Rating(int(a), int(k), float(s)) for a, s in zip(ri, rs)])
+        return [(int(k), [Rating(int(a), int(k), float(s)) for a, s in zip(ri, rs)
+                          if np.isfinite(s)])
                 for k, ri, rs in zip(keys, ids, sc)]
 
 

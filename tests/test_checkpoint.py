@@ -25,10 +25,10 @@ class _Eng:
     def fingerprint(self):
         return dict(self.data)
 
-    def user_factors(self):
+    def user_factors(self, cache=True):
         return torch.as_tensor(self.ids), torch.as_tensor(self.U)
 
-    def item_factors(self):
+    def item_factors(self, cache=True):
         return torch.arange(self.V.shape[0], dtype=torch.int32), torch.as_tensor(self.V)
 
     def check_status(self):
@@ -57,6 +57,52 @@ def test_save_interval_and_round_trip(tmp_path):
     assert not [f for f in os.listdir(d) if ".tmp" in f]
     C.maybe_save(d, -1, 4, e, 3, 0.1, False, 1.0)  # checkpointInterval -1: disabled
     assert C.load(d).iteration == 3
+    C.maybe_save(d, 3, 6, _eng(1), 3, 0.1, False, 1.0)  # a new generation replaces the old
+    assert C.load(d).iteration == 6
+    assert len([f for f in os.listdir(d) if f.startswith("gen-")]) == 1
+
+
+def test_save_killed_before_commit_keeps_previous_state(tmp_path, monkeypatch):
+    """A save that dies after writing the new generation's files but before the JSON
+    commit leaves the previous checkpoint whole: its iteration AND its factors."""
+    d = str(tmp_path / "ck")
+    old = _eng(0)
+    C.maybe_save(d, 2, 2, old, 3, 0.1, False, 1.0, init={"seed": 1})
+    real_replace = os.replace
+
+    def dying_replace(src, dst):
+        if dst.endswith(C.STATE):
+            raise KeyboardInterrupt("killed before the commit")
+        return real_replace(src, dst)
+
+    monkeypatch.setattr(C.os, "replace", dying_replace)
+    with pytest.raises(KeyboardInterrupt):
+        C.maybe_save(d, 2, 4, _eng(5), 3, 0.1, False, 1.0, init={"seed": 1})
+    monkeypatch.setattr(C.os, "replace", real_replace)
+    st = C.load(d)
+    assert st.iteration == 2
+    np.testing.assert_array_equal(st.U, old.U)
+    np.testing.assert_array_equal(st.V, old.V)
+    # the next completed save commits and clears the orphaned generation
+    C.maybe_save(d, 2, 4, _eng(5), 3, 0.1, False, 1.0, init={"seed": 1})
+    assert C.load(d).iteration == 4
+    assert len([f for f in os.listdir(d) if f.startswith("gen-")]) == 1
+    assert not [f for f in os.listdir(d) if f.endswith(".tmp")]
+
+
+def test_auto_resume_requires_the_same_initialisation(tmp_path):
+    """Spark: a checkpoint dir never changes the model.  "auto" resumes only a fit with
+    the same seed (or the same explicit U0); resume=True continues regardless."""
+    e = _eng()
+    d = str(tmp_path / "ck")
+    C.maybe_save(d, 2, 2, e, 3, 0.1, False, 1.0, init=C.init_key(7, None))
+    assert C.resume_point(d, "auto", e, 3, 0.1, False, 1.0, 10, C.init_key(7, None))[0] == 2
+    assert C.resume_point(d, "auto", e, 3, 0.1, False, 1.0, 10, C.init_key(8, None)) == \
+        (0, None, None)
+    U0 = np.ones((4, 3), np.float32)
+    assert C.resume_point(d, "auto", e, 3, 0.1, False, 1.0, 10, C.init_key(7, U0)) == \
+        (0, None, None)
+    assert C.resume_point(d, True, e, 3, 0.1, False, 1.0, 10, C.init_key(8, None))[0] == 2
 
 
 def test_resume_point_rules(tmp_path):

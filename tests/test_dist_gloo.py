@@ -264,14 +264,23 @@ def _resume_worker(rank, world, port, out_dir, mode):
     sel = np.arange(len(u)) % world == rank
     K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
     ck = os.path.join(out_dir, "ckpt")
+    # resumes read the checkpoint on process 0 only (rank 1 is given an empty directory:
+    # no shared filesystem) and broadcast the decision and the factors
+    ck_r = ck if rank == 0 else os.path.join(out_dir, f"empty_{mode}_{rank}")
     if mode == "full":
         K.fit(5, 4, 0.1, seed=7)
+    elif mode == "fresh99":
+        K.fit(5, 4, 0.1, seed=99)
     elif mode == "ckpt":
         K.fit(5, 2, 0.1, seed=7, checkpoint_dir=ck, checkpoint_interval=2)
     elif mode == "resume":
-        K.fit(5, 4, 0.1, seed=99, checkpoint_dir=ck, checkpoint_interval=0, resume=True)
+        K.fit(5, 4, 0.1, seed=99, checkpoint_dir=ck_r, checkpoint_interval=0, resume=True)
+    elif mode == "auto7":  # same seed: "auto" resumes
+        K.fit(5, 4, 0.1, seed=7, checkpoint_dir=ck_r, checkpoint_interval=0, resume="auto")
+    elif mode == "auto99":  # other seed: a different fit, "auto" starts fresh
+        K.fit(5, 4, 0.1, seed=99, checkpoint_dir=ck_r, checkpoint_interval=0, resume="auto")
     else:  # "at": nothing left to run, U and V come from the checkpoint
-        K.fit(5, 2, 0.1, seed=99, checkpoint_dir=ck, checkpoint_interval=0, resume=True)
+        K.fit(5, 2, 0.1, seed=99, checkpoint_dir=ck_r, checkpoint_interval=0, resume=True)
     _, Uf = K.user_factors()
     _, Vf = K.item_factors()
     if rank == 0:
@@ -281,18 +290,27 @@ def _resume_worker(rank, world, port, out_dir, mode):
 
 def test_checkpoint_resume_across_world_sizes(tmp_path):
     """A fit checkpointed at iteration 2 on 1 rank and resumed to 4 on 2 ranks gives
-    the uninterrupted 4-iteration factors (the resume's own seed is ignored)."""
-    for mode, world in (("full", 2), ("ckpt", 1), ("resume", 2), ("at", 2)):
+    the uninterrupted 4-iteration factors: with resume=True the resume's own seed is
+    ignored; with "auto" the seed must match (another seed is another fit and starts
+    fresh).  Only process 0 sees the checkpoint; every rank resumes alike."""
+    from als_mi355x import checkpoint as C
+    for mode, world in (("full", 2), ("fresh99", 2), ("ckpt", 1), ("resume", 2), ("at", 2),
+                        ("auto7", 2), ("auto99", 2)):
         mp.spawn(_resume_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world,
                  join=True)
     full = np.load(tmp_path / "full_w2.npz")
-    res = np.load(tmp_path / "resume_w2.npz")
-    np.testing.assert_array_equal(res["U"], full["U"])
-    np.testing.assert_array_equal(res["V"], full["V"])
-    ck = np.load(tmp_path / "ckpt" / "user_factors.npy")
+    for mode in ("resume", "auto7"):
+        res = np.load(tmp_path / f"{mode}_w2.npz")
+        np.testing.assert_array_equal(res["U"], full["U"])
+        np.testing.assert_array_equal(res["V"], full["V"])
+    a99 = np.load(tmp_path / "auto99_w2.npz")
+    np.testing.assert_array_equal(a99["U"], np.load(tmp_path / "fresh99_w2.npz")["U"])
+    assert not np.array_equal(a99["U"], full["U"])
+    st = C.load(str(tmp_path / "ckpt"))
+    assert st.iteration == 2 and st.init == {"seed": 7}
     at = np.load(tmp_path / "at_w2.npz")
-    np.testing.assert_array_equal(at["U"], ck)
-    np.testing.assert_array_equal(at["V"], np.load(tmp_path / "ckpt" / "item_factors.npy"))
+    np.testing.assert_array_equal(at["U"], st.U)
+    np.testing.assert_array_equal(at["V"], st.V)
 
 
 def _surface_worker(rank, world, port, out_dir):

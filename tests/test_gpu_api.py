@@ -180,3 +180,39 @@ def test_engine_ids_beyond_compact_range():
     ids, _ = shifted.user_factors()
     assert int(ids.min()) == int(u.min()) + 2_000_000_000 - 200
     assert torch.isnan(shifted.predict([0], [0])).all()
+
+
+def test_topk_non_finite_factors_leave_no_bogus_ids():
+    """Scores involving a NaN factor row are NaN; the kernel never ranks them, so a query
+    row with NaN factors gets no recommendations (empty slots, score -inf) and a NaN item
+    is never recommended.  The ml / mllib surfaces drop the empty slots instead of
+    turning their placeholder index into an id."""
+    rng = np.random.default_rng(4)
+    U = rng.normal(size=(40, 12)).astype(np.float32)
+    V = rng.normal(size=(30, 12)).astype(np.float32)
+    U[5] = np.nan
+    V[7] = np.nan
+    uids = np.arange(40, dtype=np.int32) * 2 - 11   # negative ids included
+    iids = np.arange(30, dtype=np.int32) * 3 + 1
+    core = E.ALSCore.from_factors(uids, U, iids, V, device=DEV)
+    keys, ids, sc = core.recommend_all(10, True)
+    sc = sc.cpu().numpy()
+    ids = ids.cpu().numpy()
+    assert np.all(np.isneginf(sc[5]))
+    ok = np.isfinite(sc)
+    assert ok[np.arange(40) != 5].all()
+    assert not np.any(ids[ok] == iids[7])
+    S = U.astype(np.float64) @ V.astype(np.float64).T
+    S[:, 7] = -np.inf
+    for t in range(40):
+        if t == 5:
+            continue
+        ref = np.lexsort((np.arange(30), -S[t]))[:10]
+        np.testing.assert_array_equal(ids[t], iids[ref])
+    model = mllib.MatrixFactorizationModel(core)
+    assert model.recommendProducts(int(uids[5]), 10) == []
+    recs = dict(model.recommendProductsForUsers(10))
+    assert recs[int(uids[5])] == [] and len(recs[int(uids[0])]) == 10
+    from als_mi355x.ml.recommendation import ALSModel
+    lists = ALSModel._recs_df("user", *core.recommend_all(10, True))
+    assert lists.loc[lists["user"] == uids[5], "recommendations"].iloc[0] == []

@@ -18,7 +18,7 @@ if [ ${#BARGS[@]} -gt 0 ] && [ "${BARGS[0]}" != "nobench" ]; then
   timeout -k 10 600 python bench.py "${BARGS[@]}" > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
   python3 -c "
 import json; d=json.load(open('$OUT/bench.json'))
-print('value', d['value'], 'ms', d['ms_per_step'])
+print('value', d.get('value'), 'ms', d.get('ms_per_step'))
 for k in ('configs2','configs3','configs4'):
     if k in d: print(k, json.dumps(d[k])[:600])
 "

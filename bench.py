@@ -571,7 +571,8 @@ def big_distributed(args, dev, rank, world):
            "n_users": sh.n_users, "n_items": sh.n_items, "nnz": sh.nnz, "rank": k,
            "ratings_per_s": sh.nnz / (t / steps), "ms_per_iter": 1e3 * t / steps,
            "steps": steps, "warmup": 1, "datagen_s": t_gen, "build_s": t_build,
-           "scaling": "strong", "n_gpus": world, "chunks": sh.users.chunks}
+           "scaling": "strong", "n_gpus": world, "chunks": sh.users.chunks,
+           "exchange": sh.exchange_stats(k)}
     # configs[4]: each rank scores its own users (every chunk of its range) against the
     # replicated V; time = max over ranks
     Vd = sh._dense(False)
@@ -614,10 +615,12 @@ def run_distributed(args):
     k = args.rank
     sh.init_factors(k, seed=5)
     t_total = _timed_iterations(sh, args.reg, args.warmup, args.steps, dev)
+    ex = sh.exchange_stats(k)
     out = None
     if rank == 0:
         out = {
             "metric": "ratings/sec per ALS iteration (rank 64)",
+            "exchange": ex,
             "value": sh.nnz / (t_total / args.steps),
             "unit": "ratings/s",
             "n_gpus": world,

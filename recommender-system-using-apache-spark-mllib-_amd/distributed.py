@@ -103,23 +103,51 @@ class HipKernels:
 
 # Largest message of one collective call.  The factor all-gathers and the one-time
 # rating routing at configs[3] scale move several GB per call; every call is kept
-# at or below this (an int32 element/byte count anywhere in a transport would
-# otherwise overflow at 2 GiB).
+# at or below this, and _guard() refuses a call above it before it is issued.
+# (The round-2 fault: at 1e9 ratings on one rank the uncapped routing all_to_all
+# moved 1e9 int32 = 4.0e9 bytes per call — 1e9 elements is below 2^31, the byte
+# count 4.0e9 is above 2^31 - 1 — and faulted inside RCCL; capped at 1 GiB the same
+# routing runs.  DESIGN.md §6.)
 MAX_COLLECTIVE_BYTES = 1 << 30
+# Row weight in ratings-equivalents for the range balance: a row's solve costs as
+# much as the Gram of a few hundred ratings, so ranges balance deg + ROW_WEIGHT.
+ROW_WEIGHT = 256
+# No range holds more than PAD_CAP x the mean rows per range: the replicated factor
+# tables and the all-gathers are padded to the largest range.
+PAD_CAP = 1.25
 
 
-def _ranges(deg: torch.Tensor, world: int):
-    """Contiguous nnz-balanced row ranges: start[w] .. start[w+1]."""
+def _guard(nbytes: int, what: str) -> None:
+    """Refuse a collective above MAX_COLLECTIVE_BYTES (every rank computes the same
+    sizes, so every rank raises before any of them issues the call)."""
+    if nbytes > MAX_COLLECTIVE_BYTES:
+        raise RuntimeError(f"{what}: {nbytes} bytes in one collective call exceeds "
+                           f"MAX_COLLECTIVE_BYTES = {MAX_COLLECTIVE_BYTES} (use more chunks)")
+
+
+def _ranges(deg: torch.Tensor, parts: int, cap_rows: Optional[int] = None):
+    """Contiguous row ranges start[w] .. start[w+1], w < parts, balancing deg + ROW_WEIGHT
+    (no row is split), with at most cap_rows rows per range (default ceil(PAD_CAP x
+    n / parts)) — when row ids correlate with popularity, pure nnz balance would give
+    the tail range most of the rows and every replicated table that padding."""
     n = deg.numel()
-    cum = torch.cumsum(deg.to(torch.float64), 0)
+    if cap_rows is None:
+        cap_rows = math.ceil(PAD_CAP * n / parts) if n else 1
+    cap_rows = max(int(cap_rows), 1)
+    w8 = deg.to(torch.float64) + float(ROW_WEIGHT)
+    cum = torch.cumsum(w8, 0)
     total = float(cum[-1]) if n else 0.0
-    targets = torch.tensor([total * w / world for w in range(1, world)], dtype=torch.float64,
+    targets = torch.tensor([total * w / parts for w in range(1, parts)], dtype=torch.float64,
                            device=deg.device)
-    cut = torch.searchsorted(cum, targets, right=True) if n else torch.zeros(world - 1)
-    starts = torch.cat([torch.zeros(1, device=deg.device, dtype=torch.long), cut.long(),
-                        torch.full((1,), n, device=deg.device, dtype=torch.long)])
-    starts = torch.maximum(starts, torch.cummax(starts, 0).values)
-    return starts.cpu()
+    cut = (torch.searchsorted(cum, targets, right=True) if n else
+           torch.zeros(parts - 1, dtype=torch.long)).cpu().tolist()
+    starts = [0]
+    for w in range(1, parts):
+        lo = max(starts[-1], n - (parts - w) * cap_rows)  # the rest must fit the rest
+        hi = min(starts[-1] + cap_rows, n)
+        starts.append(min(max(int(cut[w - 1]), lo), hi))
+    starts.append(n)
+    return torch.tensor(starts, dtype=torch.long)
 
 
 @dataclass
@@ -173,6 +201,12 @@ class SideLayout:
 
     def chunk_rows(self, rank: int, c: int) -> int:
         return int(self.cstarts[rank, c + 1] - self.cstarts[rank, c])
+
+    @property
+    def padding(self) -> float:
+        """Rows of the replicated (padded) table / real rows (<= PAD_CAP by _ranges)."""
+        world = self.cstarts.shape[0]
+        return world * self.rows_per_rank / max(self.n, 1)
 
 
 class ShardedALS:
@@ -240,7 +274,7 @@ class ShardedALS:
         least enough chunks that one chunk's all-gather (all ranks, rank <= 128
         factors, 512 B per row) stays within MAX_COLLECTIVE_BYTES."""
         big = max(u_space, i_space)
-        need = -(-big * 512 // MAX_COLLECTIVE_BYTES)
+        need = math.ceil(PAD_CAP * big * 512 / MAX_COLLECTIVE_BYTES)
         if self.world == 1:
             return max(1, need)
         return max(4 if big // self.world >= (1 << 20) else 1, need)
@@ -258,7 +292,10 @@ class ShardedALS:
         dist.all_reduce(deg, group=self.group)
         starts = _ranges(deg, self.world)
         degc = deg.cpu()
-        cst = torch.stack([_ranges(degc[int(starts[w]):int(starts[w + 1])], self.chunks)
+        # chunk ranges capped against the GLOBAL mean rows per (rank, chunk), so the
+        # padded chunk stays within PAD_CAP of it too
+        cap_c = max(1, math.ceil(PAD_CAP * n / (self.world * self.chunks)))
+        cst = torch.stack([_ranges(degc[int(starts[w]):int(starts[w + 1])], self.chunks, cap_c)
                            + starts[w] for w in range(self.world)])
         rpc = max(int((cst[:, 1:] - cst[:, :-1]).max()), 1)
         return SideLayout(n, starts, cst, rpc, dmap, uniq, offset)
@@ -299,6 +336,7 @@ class ShardedALS:
         W = self.world
         o = torch.empty(sum(rc), dtype=t.dtype, device=t.device)
         per = max(1, MAX_COLLECTIVE_BYTES // (t.element_size() * W))
+        _guard(min(per, max(max(sc), max(rc), 1)) * W * t.element_size(), "routing all_to_all")
         rounds_t = torch.tensor([-(-max(max(sc), max(rc), 1) // per)], dtype=torch.int64,
                                 device=dev)
         dist.all_reduce(rounds_t, op=dist.ReduceOp.MAX, group=self.group)
@@ -361,6 +399,7 @@ class ShardedALS:
             self.U_loc[c, :b - a, :rank] = x[a:b]
         del x
         full = self.U_full.view(us.chunks, -1, ld)
+        _guard(full[0].numel() * full.element_size(), "factor all_gather")
         for c in range(us.chunks):
             dist.all_gather_into_tensor(full[c], self.U_loc[c], group=self.group)
 
@@ -373,6 +412,7 @@ class ShardedALS:
     def _solve_and_gather(self, blocks, Y_full, X_loc, X_full, reg, implicit, alpha, yty):
         """Solve chunk c, start its all-gather, go on with chunk c+1; wait at the end."""
         Xf = X_full.view(X_loc.shape[0], -1, X_full.shape[1])
+        _guard(Xf[0].numel() * Xf.element_size(), "factor all_gather")
         works = []
         first = True
         for c, blk in enumerate(blocks):
@@ -454,6 +494,19 @@ class ShardedALS:
 
     def user_factor_ids(self) -> torch.Tensor:
         return self.users.ids()
+
+    def exchange_stats(self, rank: Optional[int] = None) -> dict:
+        """Padding of the replicated tables and the all-gather bytes one rank receives
+        per ALS iteration (both factor halves), at factor rank `rank` (ld = rank
+        rounded to 4)."""
+        k = self.rank if rank is None else rank
+        ld = (k + 3) // 4 * 4
+        W = self.world
+        recv = sum((W - 1) * s.rows_per_rank * ld * 4 for s in (self.users, self.items))
+        return {"padding_users": self.users.padding, "padding_items": self.items.padding,
+                "rows_per_chunk": [self.users.rows_per_chunk, self.items.rows_per_chunk],
+                "chunks": [self.users.chunks, self.items.chunks],
+                "allgather_recv_bytes_per_iter": recv}
 
     # ---- serving protocol (engine.ALSCore's), on the replicated factors ----
     def _dense(self, user_side: bool, cache: bool = True) -> torch.Tensor:

@@ -223,14 +223,14 @@ def _route_worker(rank, world, port, out_dir):
     u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
     sel = np.arange(len(u)) % world == rank
     ref = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=2)
+    ref.fit(4, 2, 0.1, seed=3)
     Dm.MAX_COLLECTIVE_BYTES = 64  # forces many routing rounds and many chunks
     small = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
     ok = small.chunks >= 2
     for a, b in ((ref.user_blocks, small.user_blocks), (ref.item_blocks, small.item_blocks)):
         ok = ok and sum(x[0][-1] for x in a if x is not None) == \
             sum(x[0][-1] for x in b if x is not None)
-    small.fit(4, 2, 0.1, U0_global=None, seed=3)
-    ref.fit(4, 2, 0.1, seed=3)
+    small.fit(4, 2, 0.1, U0_global=None, seed=3)  # every call within the 64-byte cap
     _, Ua = ref.user_factors()
     _, Ub = small.user_factors()
     np.save(os.path.join(out_dir, f"route_{rank}.npy"),
@@ -378,3 +378,111 @@ def test_ml_and_mllib_surface_on_sharded_engine(tmp_path):
     np.testing.assert_array_equal(np.sort(users), uids)
     order = np.argsort(users)
     np.testing.assert_array_equal(items[order], iids[ref_i])
+
+
+def test_ranges_cap_padding_with_popularity_ordered_ids():
+    """Row ids that correlate with popularity (unpermuted Zipf: id 0 the most popular)
+    make pure nnz balance hand the last range most of the rows; the ranges are capped
+    at PAD_CAP x the mean rows, so the replicated (padded) tables stay within 1.25x."""
+    import math
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x import distributed as Dm
+    n = 1_000_000
+    p = 1.0 / np.arange(1, n + 1) ** 0.9
+    deg = torch.as_tensor(np.maximum(1, np.round(1e9 * p / p.sum())).astype(np.int64))
+    for parts in (2, 4, 8):
+        st = Dm._ranges(deg, parts)
+        rows = (st[1:] - st[:-1]).numpy()
+        assert rows.sum() == n and st[0] == 0 and st[-1] == n
+        assert rows.max() <= math.ceil(Dm.PAD_CAP * n / parts)
+        assert parts * rows.max() / n <= Dm.PAD_CAP + 1e-6
+        # uncapped nnz balance would have padded far more
+        old = np.searchsorted(np.cumsum(deg.numpy()), [deg.sum().item() * w / parts
+                                                       for w in range(1, parts)], side="right")
+        old_rows = np.diff(np.concatenate([[0], old, [n]]))
+        assert parts * old_rows.max() / n > 1.5
+
+
+def _padding_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x.distributed import ShardedALS
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(8)
+    n_u, n_i = 400, 300
+    # popularity follows the id: Zipf over item ids, user degrees decreasing with id
+    pi = 1.0 / np.arange(1, n_i + 1) ** 0.9
+    pi /= pi.sum()
+    du = np.maximum(2, (60 / np.arange(1, n_u + 1) ** 0.5).astype(int))
+    us, its = [], []
+    for uid in range(n_u):
+        its.append(rng.choice(n_i, min(du[uid], n_i), replace=False, p=pi))
+        us.append(np.full(len(its[-1]), uid))
+    u = np.concatenate(us).astype(np.int32)
+    i = np.concatenate(its).astype(np.int32)
+    # every item rated at least once
+    miss = np.setdiff1d(np.arange(n_i), i)
+    u = np.concatenate([u, rng.integers(0, n_u, len(miss))]).astype(np.int32)
+    i = np.concatenate([i, miss]).astype(np.int32)
+    r = np.clip(np.round(rng.normal(3.5, 1.0, len(u)) * 2) / 2, 0.5, 5).astype(np.float32)
+    sel = np.arange(len(u)) % world == rank
+    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=2)
+    from oracle import als_oracle as O
+    U0 = O.initialize(len(np.unique(u)), 5, seed=3)
+    K.fit(5, 2, 0.1, U0_global=U0)
+    _, Uf = K.user_factors()
+    ex = K.exchange_stats()
+    if rank == 0:
+        U_ref, *_ = O.train(u, i, r, 5, 2, 0.1, U0=U0)
+        np.save(os.path.join(out_dir, f"pad_{world}.npy"),
+                np.array([ex["padding_users"], ex["padding_items"],
+                          float(np.abs(Uf.numpy() - U_ref).max())]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_padding_bounded_with_popularity_ordered_ids(tmp_path, world):
+    mp.spawn(_padding_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    pu, pi, diff = np.load(tmp_path / f"pad_{world}.npy")
+    assert pu <= 1.25 + 1e-9 and pi <= 1.25 + 1e-9, (pu, pi)
+    assert diff <= 1e-4
+
+
+def _guard_worker(rank, world, port, out_dir):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x import distributed as Dm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    u, i, r = planted(120, 90, density=0.08, seed=21)
+    sel = np.arange(len(u)) % world == rank
+    K = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=1)
+    Dm.MAX_COLLECTIVE_BYTES = 256  # one chunk's factor all-gather is larger than this
+    msg = ""
+    try:
+        K.fit(8, 1, 0.1, seed=1)
+    except RuntimeError as e:
+        msg = str(e)
+    np.save(os.path.join(out_dir, f"guard_{rank}.npy"), np.array([float("MAX_COLLECTIVE" in msg)]))
+    dist.destroy_process_group()
+
+
+def test_collective_size_guard_refuses_oversized_calls(tmp_path):
+    """Every collective is checked against MAX_COLLECTIVE_BYTES before it is issued;
+    an oversized all-gather (one chunk, forced) raises on every rank instead of
+    reaching the transport."""
+    mp.spawn(_guard_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for w in range(2):
+        assert np.load(tmp_path / f"guard_{w}.npy")[0] == 1.0

@@ -512,13 +512,17 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
   // sub-list of row m (every lane: sub-list q)
   constexpr bool QUAD = TOPR > 16;
-  static_assert(!QUAD || (RG == 1 && TOPR % 4 == 0), "quad lists: one row group");
+  static_assert(!QUAD || TOPR % 4 == 0, "quad lists: TOPR divisible by 4");
   // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
   constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
+  constexpr int NL = QUAD ? RG : 1;  // lists per lane: quad, one sub-list per row group
   const int ncap = QUAD ? top / 4 + (q < top % 4 ? 1 : 0) : top;  // live slots of this list
-  uint64_t kv[NR];
+  uint64_t kvs[NL][NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) kv[j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
+  for (int g = 0; g < NL; ++g)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) kvs[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
+  uint64_t (&kv)[NR] = kvs[0];
 
   uint4 pre[PER];
   int pre_p = 0x7fffffff;
@@ -598,26 +602,32 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
       asm volatile("" ::: "memory");  // LDS is in order within the wave
       if constexpr (QUAD) {
-        // every lane: sub-list q of row m; one candidate per row per pass
+        // every lane: sub-list q of row m of each row group; one candidate per row
+        // per pass
         const int rho = m;
-        uint64_t bb = b[0][0];
 #pragma unroll
-        for (int t = 1; t < 4; ++t) bb = (rho & 3) == t ? b[0][t] : bb;
-        unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
-        const float* sg = st + rho;
-        while (__ballot(msk != 0)) {
-          const bool act = msk != 0;
-          const int mm = act ? __builtin_ctz(msk) : 0;
-          msk &= msk - 1;
-          const float sc = sg[16 * mm];
-          const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
-          const uint64_t gmin = tk_quad_min(kv[0]);
-          // the lowest sub-list whose [0] is the row minimum takes the candidate
-          const uint64_t holders = (__ballot(kv[0] == gmin) >> rho) & 0x0001000100010001ull;
-          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv, c);
+        for (int g = 0; g < RG; ++g) {
+          uint64_t bb = b[g][0];
+#pragma unroll
+          for (int t = 1; t < 4; ++t) bb = (rho & 3) == t ? b[g][t] : bb;
+          unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
+          const float* sg = st + g * 256 + rho;
+          while (__ballot(msk != 0)) {
+            const bool act = msk != 0;
+            const int mm = act ? __builtin_ctz(msk) : 0;
+            msk &= msk - 1;
+            const float sc = sg[16 * mm];
+            const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
+            const uint64_t gmin = tk_quad_min(kvs[g][0]);
+            // the lowest sub-list whose [0] is the row minimum takes the candidate
+            const uint64_t holders =
+                (__ballot(kvs[g][0] == gmin) >> rho) & 0x0001000100010001ull;
+            if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kvs[g], c);
+          }
+          const uint64_t gmin = tk_quad_min(kvs[g][0]);
+          if (q == 0)
+            thr[16 * g + rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
         }
-        const uint64_t gmin = tk_quad_min(kv[0]);
-        if (q == 0) thr[rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
       } else if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
         const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
         uint64_t bb = b[0][0];
@@ -643,9 +653,15 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? t4[r] : __builtin_inff();
       }
       if (!full) {
-        const bool open_list =
-            QUAD ? (((live[0] >> m) & 1u) && kv[0] == kTkKeyOpen)
-                 : (lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) && kv[0] == kTkKeyOpen);
+        bool open_list = false;
+        if constexpr (QUAD) {
+#pragma unroll
+          for (int g = 0; g < RG; ++g)
+            open_list = open_list || (((live[g] >> m) & 1u) && kvs[g][0] == kTkKeyOpen);
+        } else {
+          open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
+                      kv[0] == kTkKeyOpen;
+        }
         full = __ballot(open_list) == 0;
       }
       return;
@@ -704,59 +720,64 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   if constexpr (QUAD) {
     // output position of a real entry = number of real entries above it in the
     // row's four sub-lists; open slots (fewer than `top` V rows) fill the tail
-    const int64_t row = qbase + 16 * w + m;
-    const bool zero = !((live[0] >> m) & 1u);
-    int rank[NR];
-    int nreal = 0, nopen = 0;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      nreal += (kv[i] != kTkKeyOpen && kv[i] != kTkKeySentinel) ? 1 : 0;
-      nopen += (i < ncap && kv[i] == kTkKeyOpen) ? 1 : 0;
-    }
+    for (int g = 0; g < RG; ++g) {
+      const uint64_t (&kl)[NR] = kvs[g];
+      const int64_t row = qbase + 64 * g + 16 * w + m;
+      const bool zero = !((live[g] >> m) & 1u);
+      int rank[NR];
+      int nreal = 0, nopen = 0;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      rank[i] = 0;
-#pragma unroll
-      for (int t = i + 1; t < NR; ++t) rank[i] += kv[t] != kTkKeySentinel ? 1 : 0;
-    }
-    auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
-      constexpr int P = decltype(pc)::value;
-#pragma unroll
-      for (int t = 0; t < NR; ++t) {
-        const uint64_t o = P == 1 ? tk_partner64<16>(kv[t])
-                                  : (P == 2 ? tk_partner64<32>(kv[t])
-                                            : tk_partner64<32>(tk_partner64<16>(kv[t])));
-        if (o != kTkKeySentinel) {
-#pragma unroll
-          for (int i = 0; i < NR; ++i) rank[i] += o > kv[i] ? 1 : 0;
-        }
+      for (int i = 0; i < NR; ++i) {
+        nreal += (kl[i] != kTkKeyOpen && kl[i] != kTkKeySentinel) ? 1 : 0;
+        nopen += (i < ncap && kl[i] == kTkKeyOpen) ? 1 : 0;
       }
-    };
-    count_above(std::integral_constant<int, 1>{});
-    count_above(std::integral_constant<int, 2>{});
-    count_above(std::integral_constant<int, 3>{});
-    const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
-    const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
-    const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
-    const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
-    const int R = nreal + r1 + r2 + r3;
-    const int obase = R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
-    if (row < n_q) {
-      if (zero) {  // every score 0: the first `top` rows, ties by index
-        if (q == 0) {
-          for (int e = 0; e < top; ++e) {
-            idx_out[row * top + e] = e < n_v ? e : -1;
-            score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        rank[i] = 0;
+#pragma unroll
+        for (int t = i + 1; t < NR; ++t) rank[i] += kl[t] != kTkKeySentinel ? 1 : 0;
+      }
+      auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
+        constexpr int P = decltype(pc)::value;
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+          const uint64_t o = P == 1 ? tk_partner64<16>(kl[t])
+                                    : (P == 2 ? tk_partner64<32>(kl[t])
+                                              : tk_partner64<32>(tk_partner64<16>(kl[t])));
+          if (o != kTkKeySentinel) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) rank[i] += o > kl[i] ? 1 : 0;
           }
         }
-      } else {
+      };
+      count_above(std::integral_constant<int, 1>{});
+      count_above(std::integral_constant<int, 2>{});
+      count_above(std::integral_constant<int, 3>{});
+      const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
+      const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
+      const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
+      const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
+      const int R = nreal + r1 + r2 + r3;
+      const int obase =
+          R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
+      if (row < n_q) {
+        if (zero) {  // every score 0: the first `top` rows, ties by index
+          if (q == 0) {
+            for (int e = 0; e < top; ++e) {
+              idx_out[row * top + e] = e < n_v ? e : -1;
+              score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+            }
+          }
+        } else {
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          if (i < ncap) {
-            const bool real = kv[i] != kTkKeyOpen;
-            const int64_t e = row * top + (real ? rank[i] : obase + i);
-            idx_out[e] = real ? tk_key_index(kv[i]) : -1;
-            score_out[e] = real ? tk_key_score(kv[i]) * unscale : -__builtin_inff();
+          for (int i = 0; i < NR; ++i) {
+            if (i < ncap) {
+              const bool real = kl[i] != kTkKeyOpen;
+              const int64_t e = row * top + (real ? rank[i] : obase + i);
+              idx_out[e] = real ? tk_key_index(kl[i]) : -1;
+              score_out[e] = real ? tk_key_score(kl[i]) * unscale : -__builtin_inff();
+            }
           }
         }
       }
@@ -819,7 +840,7 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 // at rank 128: one 120 KB workgroup per CU 602 ms, two 68 KB ones 480 ms).
 static int topk_split_rg(int k, int top, bool quad) {
   const int kq = topk_kq(k);
-  if (quad) return 1;  // quad lists: one row group
+  if (quad) return 2;  // quad lists: two row groups (each V tile feeds 128 query rows)
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
   if (topk_split_lds_bytes(kq, 1, top, false) <= (size_t)kLdsBytes) return 1;
@@ -917,16 +938,14 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
     else if (!quad)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
-    else if (RG != 1)                                 \
-      return ALS_EUNSUPPORTED;                        \
     else if (top <= 32)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 32);              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 32);             \
     else if (top <= 64)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 64);              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 64);             \
     else if (top <= 100)                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 100);             \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 100);            \
     else                                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, kTopQ);           \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopQ);          \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);

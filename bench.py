@@ -233,8 +233,8 @@ def topk_variant(k: int, top: int) -> str:
     nk = max(32, kp_of(k)) // 32
     if top <= 16:
         rg, tr = 2, (8 if top <= 8 else (12 if top <= 12 else 16))
-    elif top <= 128:  # quad register lists, two row groups
-        rg, tr = 2, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
+    elif top <= 128:  # quad register lists, one row group
+        rg, tr = 1, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
     else:
         return f"topk_split_kernel<{nk},?,0,0>"
     return f"topk_split_kernel<{nk},{rg},{tr},0>"

@@ -33,7 +33,6 @@
 #include "als_common.h"
 
 #include <algorithm>
-#include <utility>
 
 namespace als {
 
@@ -348,11 +347,12 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // Split-f16 scores.  NK = KQ / 32 MFMA k-steps (KQ = k padded to 32, 64 or 128);
 // RG query-row groups of 64 per workgroup.  scal[0] = max |Q|, scal[1] = max |V|.
 //
-// V is swept in tiles of tk_vt_q(NK) rows through three LDS buffers filled by
-// LDS-DMA (global_load_lds_dwordx4): ONE barrier per tile, the DMAs of the next two
-// tiles in flight while a tile is scored, and no VGPRs spent on staging.  Tile rows
-// are stored swizzled (tk_swz), which keeps the ds_read_b128 B-operand reads
-// conflict-free without padding (a DMA writes its 1 KB lane-linearly).
+// V is swept in tiles of kTkVT(NK) rows, double-buffered in LDS: tile t+1 is
+// written (from registers loaded one tile earlier) while nothing reads its
+// buffer, so ONE barrier per tile; the global loads of tile t+2 are then in
+// flight during tile t+1's MFMAs.  LDS rows are RW + 2 uint4 apart: the
+// ds_read_b128 lane groups of gfx950 ({0-3,12-15,20-27}, ...) then touch 16
+// distinct 4-bank slots (row stride = 2 mod 16 slots), conflict-free.
 // Filter: the (score, index) k-th of a full list always has a smaller index than
 // the V rows being scored (V is swept in index order), so a candidate can beat
 // it only if score >= k-th score: one compare per score, one ballot per 16 x 16
@@ -387,26 +387,6 @@ __host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
 __host__ __device__ constexpr int tk_vt_q(int nk, bool quad) {
   return quad ? (nk == 1 ? 2 : 4) * tk_vt(nk) : tk_vt(nk);
 }
-
-// Compile-time loop (the index is a constant expression in the body, so register
-// arrays indexed by it stay in registers).
-template <class F, int... I>
-__device__ __forceinline__ void tk_static_for_impl(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-template <int N, class F>
-__device__ __forceinline__ void tk_static_for(F&& f) {
-  tk_static_for_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// Row swizzle of the LDS tile image: 16-B chunk c of tile row r sits at c ^ tk_swz(r).
-// The B-operand reads (lane (q, m): row 16i + m, chunk 4s + q, and the lo half's
-// chunk) then hit 16 distinct 4-bank slots in every ds_read_b128 lane group of gfx950
-// ({0-3,12-15,20-27}, {4-11,16-19,28-31}, ...): rows are RW = 8 NK chunks, so for
-// NK >= 2 a chunk's slot is (c ^ (r & 15)) mod 16, and for NK = 1 it is
-// 8 (r & 1) + (c ^ ((r >> 1) & 7)).
-template <int NK>
-__host__ __device__ constexpr int tk_swz(int r) { return NK == 1 ? (r >> 1) & 7 : r & 15; }
 
 // Insert key `c` into a list sorted ascending (the k-th best at [0]; sentinels past
 // `top`).  c_j = c > key_j is monotone (true for j < p); the list becomes
@@ -470,16 +450,17 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
                                                          float* __restrict__ score_out) {
   constexpr int KQ = 32 * NK;
   constexpr int RW = KQ / 4;           // uint4 per split row (KQ hi + KQ lo halves)
+  constexpr int RS = RW + 2;           // LDS row stride in uint4 (bank-conflict-free)
   constexpr int VT = tk_vt_q(NK, TOPR > 16);  // V rows per tile
   constexpr int NC = VT / 16;          // 16-row score blocks per tile
   constexpr int PER = VT * RW / 256;   // staged uint4 per thread per tile
   static_assert(PER * 256 == VT * RW, "tile staging");
   extern __shared__ uint4 smem_u4[];
-  uint4* tiles = smem_u4;                                     // [3][VT][RW], swizzled rows
-  int* tperm = reinterpret_cast<int*>(tiles + 3 * VT * RW);   // [3][VT] V row of each tile row
+  uint4* tiles = smem_u4;                                     // [2][VT][RS]
+  int* tperm = reinterpret_cast<int*>(tiles + 2 * VT * RS);   // [2][VT] V row of each tile row
   // TOPR == 0: [64 RG rows][top] keys (best first), [64 RG] lengths
   // TOPR > 0: per wave and group a 16 x 16 score block [item m][row]
-  uint64_t* lk = reinterpret_cast<uint64_t*>(tperm + 3 * VT);  // 8-byte aligned: VT % 16 == 0
+  uint64_t* lk = reinterpret_cast<uint64_t*>(tperm + 2 * VT);  // 8-byte aligned: VT % 16 == 0
   int* len = reinterpret_cast<int*>(lk + 64 * RG * top);
   float* sblk = reinterpret_cast<float*>(lk);
 
@@ -531,53 +512,44 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
   // sub-list of row m (every lane: sub-list q)
   constexpr bool QUAD = TOPR > 16;
-  static_assert(!QUAD || TOPR % 4 == 0, "quad lists: TOPR divisible by 4");
+  static_assert(!QUAD || (RG == 1 && TOPR % 4 == 0), "quad lists: one row group");
   // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
   constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
-  constexpr int NL = QUAD ? RG : 1;  // lists per lane: quad, one sub-list per row group
   const int ncap = QUAD ? top / 4 + (q < top % 4 ? 1 : 0) : top;  // live slots of this list
-  uint64_t kvs[NL][NR];
+  uint64_t kv[NR];
 #pragma unroll
-  for (int g = 0; g < NL; ++g)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) kvs[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
-  uint64_t (&kv)[NR] = kvs[0];
+  for (int j = 0; j < NR; ++j) kv[j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
 
-  // Tile t of V (rows t*VT ..) -> LDS buffer buf by LDS-DMA (global_load_lds_dwordx4:
-  // wave-uniform destination, lane-linear 16-B pieces; the per-lane SOURCE address
-  // applies the row swizzle, tk_swz), plus the tile's V row indices (one 4-B DMA per
-  // wave, VT/4 lanes).  Rows past n_v read the NaN sentinel row n_v of the table, so
-  // their scores are NaN and never pass a filter.  Every wave issues PER + 1 DMAs per
-  // tile.  No VGPR holds staged data.
-  const int64_t ntiles = (n_v + VT - 1) / VT;
-  auto issue = [&](int64_t t, int buf) {
-    const int64_t vb = t * VT;
-    char* dst = reinterpret_cast<char*>(tiles + buf * VT * RW);
+  uint4 pre[PER];
+  int pre_p = 0x7fffffff;
+  auto fetch = [&](int64_t vb) {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const int p = e * 256 + w * 64 + lane;
-      const int r = p / RW, pos = p % RW;
-      const int c = pos ^ tk_swz<NK>(r);
-      const int64_t vrow = vb + r < n_v ? vb + r : n_v;
-      __builtin_amdgcn_global_load_lds(Vsp + vrow * RW + c, dst + (e * 256 + w * 64) * 16, 16, 0,
-                                       0);
+      const int x = threadIdx.x + 256 * e;
+      const int64_t vrow = vb + x / RW;
+      // rows past n_v: f16 NaNs, so their scores are NaN and never pass a filter
+      pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW]
+                          : make_uint4(0x7E007E00u, 0x7E007E00u, 0x7E007E00u, 0x7E007E00u);
     }
-    if (lane < VT / 4) {
-      const int64_t j = vb + w * (VT / 4) + lane;
-      __builtin_amdgcn_global_load_lds(perm + (j < n_v ? j : 0),
-                                       reinterpret_cast<char*>(tperm + buf * VT + w * (VT / 4)),
-                                       4, 0, 0);
-    }
+    if (threadIdx.x < VT) pre_p = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
   };
-  const int swz = tk_swz<NK>(m);  // block rows are 16c + m: the swizzle depends on m only
+  auto stage = [&](int buf) {
+    uint4* t = tiles + buf * VT * RS;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int x = threadIdx.x + 256 * e;
+      t[(x / RW) * RS + x % RW] = pre[e];
+    }
+    if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p;
+  };
   auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {
     // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
-      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[(4 * s + q) ^ swz]);
-      const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[(KQ / 8 + 4 * s + q) ^ swz]);
+      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+      const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[KQ / 8 + 4 * s + q]);
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
@@ -626,39 +598,33 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
       asm volatile("" ::: "memory");  // LDS is in order within the wave
       if constexpr (QUAD) {
-        // every lane: sub-list q of row m of each row group; one candidate per row
-        // per pass
+        // every lane: sub-list q of row m; one candidate per row per pass
         const int rho = m;
-        tk_static_for<RG>([&](auto gc) {
-          constexpr int g = decltype(gc)::value;
-          // this row's ballot among the four (wave-uniform) ones: masked merges, the
-          // masks opaque to the compiler (a select chain on a lane-varying index is
-          // otherwise turned into a private-memory table lookup)
-          uint64_t bb = b[g][0];
+        // this row's ballot among the four (wave-uniform) ones: masked merges, the
+        // masks opaque to the compiler (a select chain on a lane-varying index is
+        // otherwise turned into a private-memory table lookup)
+        uint64_t bb = b[0][0];
 #pragma unroll
-          for (int t = 1; t < 4; ++t) {
-            uint64_t sel = (rho & 3) == t ? ~0ull : 0ull;
-            asm volatile("" : "+v"(sel));
-            bb = (bb & ~sel) | (b[g][t] & sel);
-          }
-          unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
-          const float* sg = st + g * 256 + rho;
-          while (__ballot(msk != 0)) {
-            const bool act = msk != 0;
-            const int mm = act ? __builtin_ctz(msk) : 0;
-            msk &= msk - 1;
-            const float sc = sg[16 * mm];
-            const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
-            const uint64_t gmin = tk_quad_min(kvs[g][0]);
-            // the lowest sub-list whose [0] is the row minimum takes the candidate
-            const uint64_t holders =
-                (__ballot(kvs[g][0] == gmin) >> rho) & 0x0001000100010001ull;
-            if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kvs[g], c);
-          }
-          const uint64_t gmin = tk_quad_min(kvs[g][0]);
-          if (q == 0)
-            thr[16 * g + rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
-        });
+        for (int t = 1; t < 4; ++t) {
+          uint64_t sel = (rho & 3) == t ? ~0ull : 0ull;
+          asm volatile("" : "+v"(sel));
+          bb = (bb & ~sel) | (b[0][t] & sel);
+        }
+        unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
+        const float* sg = st + rho;
+        while (__ballot(msk != 0)) {
+          const bool act = msk != 0;
+          const int mm = act ? __builtin_ctz(msk) : 0;
+          msk &= msk - 1;
+          const float sc = sg[16 * mm];
+          const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
+          const uint64_t gmin = tk_quad_min(kv[0]);
+          // the lowest sub-list whose [0] is the row minimum takes the candidate
+          const uint64_t holders = (__ballot(kv[0] == gmin) >> rho) & 0x0001000100010001ull;
+          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv, c);
+        }
+        const uint64_t gmin = tk_quad_min(kv[0]);
+        if (q == 0) thr[rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
       } else if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
         const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
         uint64_t bb = b[0][0];
@@ -684,15 +650,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? t4[r] : __builtin_inff();
       }
       if (!full) {
-        bool open_list = false;
-        if constexpr (QUAD) {
-#pragma unroll
-          for (int g = 0; g < RG; ++g)
-            open_list = open_list || (((live[g] >> m) & 1u) && kvs[g][0] == kTkKeyOpen);
-        } else {
-          open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
-                      kv[0] == kTkKeyOpen;
-        }
+        const bool open_list =
+            QUAD ? (((live[0] >> m) & 1u) && kv[0] == kTkKeyOpen)
+                 : (lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) && kv[0] == kTkKeyOpen);
         full = __ballot(open_list) == 0;
       }
       return;
@@ -719,37 +679,30 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     }
   };
 
-  // Three LDS buffers, ONE raw barrier per tile, two tiles of DMAs in flight: at tile
-  // t each wave waits for its own DMAs of tile t (counted vmcnt: tile t+1's stay in
-  // flight), the barrier makes every wave's part visible and guarantees that every
-  // wave is done with tile t-1, whose buffer then receives tile t+2.
-  if (ntiles > 0) issue(0, 0);
-  if (ntiles > 1) issue(1, 1);
-  for (int64_t t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 1) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (t + 2 < ntiles) issue(t + 2, (int)((t + 2) % 3));
-    const int buf = (int)(t % 3);
-    const int64_t vb = t * VT;
-    const uint4* tb = tiles + buf * VT * RW;
+  fetch(0);
+  stage(0);
+  __syncthreads();
+  if (VT < n_v) fetch(VT);
+  int buf = 0;
+  for (int64_t vb = 0; vb < n_v; vb += VT) {
+    const uint4* tb = tiles + buf * VT * RS;
     floatx4 acc0[RG], acc1[RG];
-    score(tb + m * RW, acc0);
+    score(tb + m * RS, acc0);
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       // issue block c+1's MFMAs, then filter block c
       if (c % 2 == 0) {
-        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RW, acc1);
+        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc1);
         filter(acc0, vb + 16 * c, tperm + buf * VT + 16 * c);
       } else {
-        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RW, acc0);
+        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc0);
         filter(acc1, vb + 16 * c, tperm + buf * VT + 16 * c);
       }
     }
+    if (vb + VT < n_v) stage(buf ^ 1);
+    __syncthreads();
+    if (vb + 2 * VT < n_v) fetch(vb + 2 * VT);
+    buf ^= 1;
   }
   if constexpr (MODE != 0) {
     if (lane == 0) score_out[blockIdx.x * 4 + w] = MODE == 1 ? sink : (float)n_offer;
@@ -758,68 +711,63 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   if constexpr (QUAD) {
     // output position of a real entry = number of real entries above it in the
     // row's four sub-lists; open slots (fewer than `top` V rows) fill the tail
-    tk_static_for<RG>([&](auto gc) {
-      constexpr int g = decltype(gc)::value;
-      const uint64_t (&kl)[NR] = kvs[g];
-      const int64_t row = qbase + 64 * g + 16 * w + m;
-      const bool zero = !((live[g] >> m) & 1u);
-      int rank[NR];
-      int nreal = 0, nopen = 0;
+    const int64_t row = qbase + 16 * w + m;
+    const bool zero = !((live[0] >> m) & 1u);
+    int rank[NR];
+    int nreal = 0, nopen = 0;
 #pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        nreal += (kl[i] != kTkKeyOpen && kl[i] != kTkKeySentinel) ? 1 : 0;
-        nopen += (i < ncap && kl[i] == kTkKeyOpen) ? 1 : 0;
+    for (int i = 0; i < NR; ++i) {
+      nreal += (kv[i] != kTkKeyOpen && kv[i] != kTkKeySentinel) ? 1 : 0;
+      nopen += (i < ncap && kv[i] == kTkKeyOpen) ? 1 : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+      rank[i] = 0;
+#pragma unroll
+      for (int t = i + 1; t < NR; ++t) rank[i] += kv[t] != kTkKeySentinel ? 1 : 0;
+    }
+    auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
+      constexpr int P = decltype(pc)::value;
+#pragma unroll
+      for (int t = 0; t < NR; ++t) {
+        const uint64_t o = P == 1 ? tk_partner64<16>(kv[t])
+                                  : (P == 2 ? tk_partner64<32>(kv[t])
+                                            : tk_partner64<32>(tk_partner64<16>(kv[t])));
+        if (o != kTkKeySentinel) {
+#pragma unroll
+          for (int i = 0; i < NR; ++i) rank[i] += o > kv[i] ? 1 : 0;
+        }
       }
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        rank[i] = 0;
-#pragma unroll
-        for (int t = i + 1; t < NR; ++t) rank[i] += kl[t] != kTkKeySentinel ? 1 : 0;
-      }
-      auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
-        constexpr int P = decltype(pc)::value;
-#pragma unroll
-        for (int t = 0; t < NR; ++t) {
-          const uint64_t o = P == 1 ? tk_partner64<16>(kl[t])
-                                    : (P == 2 ? tk_partner64<32>(kl[t])
-                                              : tk_partner64<32>(tk_partner64<16>(kl[t])));
-          if (o != kTkKeySentinel) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) rank[i] += o > kl[i] ? 1 : 0;
+    };
+    count_above(std::integral_constant<int, 1>{});
+    count_above(std::integral_constant<int, 2>{});
+    count_above(std::integral_constant<int, 3>{});
+    const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
+    const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
+    const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
+    const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
+    const int R = nreal + r1 + r2 + r3;
+    const int obase = R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
+    if (row < n_q) {
+      if (zero) {  // every score 0: the first `top` rows, ties by index
+        if (q == 0) {
+          for (int e = 0; e < top; ++e) {
+            idx_out[row * top + e] = e < n_v ? e : -1;
+            score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
           }
         }
-      };
-      count_above(std::integral_constant<int, 1>{});
-      count_above(std::integral_constant<int, 2>{});
-      count_above(std::integral_constant<int, 3>{});
-      const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
-      const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
-      const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
-      const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
-      const int R = nreal + r1 + r2 + r3;
-      const int obase =
-          R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
-      if (row < n_q) {
-        if (zero) {  // every score 0: the first `top` rows, ties by index
-          if (q == 0) {
-            for (int e = 0; e < top; ++e) {
-              idx_out[row * top + e] = e < n_v ? e : -1;
-              score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
-            }
-          }
-        } else {
+      } else {
 #pragma unroll
-          for (int i = 0; i < NR; ++i) {
-            if (i < ncap) {
-              const bool real = kl[i] != kTkKeyOpen;
-              const int64_t e = row * top + (real ? rank[i] : obase + i);
-              idx_out[e] = real ? tk_key_index(kl[i]) : -1;
-              score_out[e] = real ? tk_key_score(kl[i]) * unscale : -__builtin_inff();
-            }
+        for (int i = 0; i < NR; ++i) {
+          if (i < ncap) {
+            const bool real = kv[i] != kTkKeyOpen;
+            const int64_t e = row * top + (real ? rank[i] : obase + i);
+            idx_out[e] = real ? tk_key_index(kv[i]) : -1;
+            score_out[e] = real ? tk_key_score(kv[i]) * unscale : -__builtin_inff();
           }
         }
       }
-    });
+    }
     return;
   } else if constexpr (TOPR > 0) {
     if (lane < 16 * RG) {
@@ -865,7 +813,7 @@ static bool topk_quad(int top, int64_t n_v) {
 static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
   const size_t vt = (size_t)tk_vt_q(nk, quad);
-  const size_t tiles = 16 * 3 * vt * (size_t)(kq / 4) + 4 * 3 * vt;
+  const size_t tiles = 16 * 2 * vt * (size_t)(kq / 4 + 2) + 4 * 2 * vt;
   if (top <= kTopR || quad) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
   return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
@@ -878,7 +826,7 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 // at rank 128: one 120 KB workgroup per CU 602 ms, two 68 KB ones 480 ms).
 static int topk_split_rg(int k, int top, bool quad) {
   const int kq = topk_kq(k);
-  if (quad) return 2;  // quad lists: two row groups (each V tile feeds 128 query rows)
+  if (quad) return 1;  // quad lists: one row group
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
   if (topk_split_lds_bytes(kq, 1, top, false) <= (size_t)kLdsBytes) return 1;
@@ -892,8 +840,7 @@ using namespace als;
 extern "C" {
 
 static size_t tk_table_bytes(int64_t n_v, int32_t k) {
-  // n_v split rows + the NaN sentinel row that tile rows past n_v read
-  return align_up(4 * (size_t)topk_kq(k) * (size_t)((n_v > 0 ? n_v : 0) + 1));
+  return align_up(4 * (size_t)topk_kq(k) * (size_t)(n_v > 0 ? n_v : 0));
 }
 
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top) {
@@ -955,9 +902,6 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     topk_split_table_kernel<<<(int)std::min<int64_t>(4096, (total + 255) / 256), 256, 0, st>>>(
         V, n_v, ld, k, kq_shift, scal, perm, vsp);
     ALS_LAUNCH_CHECK();
-    // sentinel row n_v: f16 NaN halves (0x7E00), scores against it are NaN
-    ALS_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(vsp + 2 * (int64_t)kq * n_v),
-                              0x7E00, 2 * (size_t)kq, st));
   }
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
   const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
@@ -980,14 +924,16 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
     else if (!quad)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
+    else if (RG != 1)                                 \
+      return ALS_EUNSUPPORTED;                        \
     else if (top <= 32)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 32);             \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 32);              \
     else if (top <= 64)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 64);             \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 64);              \
     else if (top <= 100)                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 100);            \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 100);             \
     else                                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopQ);          \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, kTopQ);           \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);

@@ -31,11 +31,11 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
       topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,  \
                                                                   k, top, scal, idx, dbg);    \
-    } else if (quad) { /* quad lists: the dev modes use 128 */                                \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, kTopQ, M>), \
+    } else if (quad) { /* quad lists (rg is 1 here): the dev modes use 100 (configs[4]) */   \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, 1, 100, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, kTopQ, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld, \
-                                                                  k, top, scal, idx, dbg);    \
+      topk_split_kernel<NK, 1, 100, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,   \
+                                                               k, top, scal, idx, dbg);       \
     } else {                                                                                  \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, 0, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \

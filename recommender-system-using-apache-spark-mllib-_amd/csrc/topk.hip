@@ -239,7 +239,8 @@ __device__ __forceinline__ int tk_row_bucket(const float* __restrict__ V, int64_
   for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if (!(s > 0.f)) return kTkBuckets - 1;
   const float b = (log2_ref - 0.5f * __log2f(s)) * 128.f;  // octaves below the reference
-  return b <= 0.f ? 0 : (b >= (float)(kTkBuckets - 1) ? kTkBuckets - 1 : (int)b);
+  // (NaN, e.g. an Inf row against an Inf reference: bucket 0)
+  return !(b > 0.f) ? 0 : (b >= (float)(kTkBuckets - 1) ? kTkBuckets - 1 : (int)b);
 }
 
 __device__ __forceinline__ float tk_log2_ref(const float* __restrict__ scal, int k) {
@@ -321,6 +322,34 @@ __global__ __launch_bounds__(256) void tk_bucket_scatter_kernel(const float* __r
   }
 }
 
+// Norms of the scaled V rows in sweep order (16 lanes per table row): the coarse
+// filter's error slack and the early-exit bound of topk_split_kernel.
+__global__ __launch_bounds__(256) void tk_table_norm_kernel(const float* __restrict__ V,
+                                                            int64_t n_v, int ld, int k,
+                                                            const float* __restrict__ scal,
+                                                            const int32_t* __restrict__ perm,
+                                                            float* __restrict__ vnorm) {
+  const float sv = ldexpf(1.f, tk_split_exponent(scal[1]));
+  const int l = threadIdx.x & 15;
+  for (int64_t t = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 4; t < n_v;
+       t += ((int64_t)gridDim.x * 256) >> 4) {
+    const int64_t r = perm[t];
+    float s = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int d = 4 * l + 64 * h;
+      if (d < k) {
+        const float4 v = *reinterpret_cast<const float4*>(V + r * ld + d);
+        s += v.x * v.x + (d + 1 < k ? v.y * v.y : 0.f) + (d + 2 < k ? v.z * v.z : 0.f) +
+             (d + 3 < k ? v.w * v.w : 0.f);
+      }
+    }
+    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    // a row with a NaN / Inf entry: an unbounded norm keeps every bound using it open
+    if (l == 0) vnorm[t] = s < __builtin_inff() ? sv * sqrtf(s) : __builtin_inff();
+  }
+}
+
 // V -> split planes in sweep order, table row t = V row perm[t]:
 // [hi(sv v[0..KQ)) | lo(sv v[0..KQ))] (f16), dims >= k zero.
 __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __restrict__ V,
@@ -353,12 +382,22 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // flight during tile t+1's MFMAs.  LDS rows are RW + 2 uint4 apart: the
 // ds_read_b128 lane groups of gfx950 ({0-3,12-15,20-27}, ...) then touch 16
 // distinct 4-bank slots (row stride = 2 mod 16 slots), conflict-free.
-// Filter: the (score, index) k-th of a full list always has a smaller index than
-// the V rows being scored (V is swept in index order), so a candidate can beat
-// it only if score >= k-th score: one compare per score, one ballot per 16 x 16
-// block; the exact (score, index) insertion runs only for blocks with a
-// survivor.  The MFMAs of block c+1 are issued before block c's filter (two
-// accumulator sets).
+// Coarse filter, exact refinement: a block is first scored with hi.hi alone (one
+// MFMA per k-step instead of three).  The dropped terms hi.lo + lo.hi are bounded
+// by 2^-10 |q| |v| (Cauchy-Schwarz on |lo| <= 2^-11 |t|, plus the f16 subnormal
+// and fp32 accumulation terms, all far below it), so a pair can reach its row's
+// k-th score only if hi.hi >= k-th - 2^-9 (|q| + 1)(|v| + 1): one fma and one
+// compare per score, one ballot per 16 x 16 block.  A block with a pair past that
+// bound gets the hi.lo + lo.hi MFMAs added (the exact score every pair is ranked
+// by, the same wherever the pair is met), then the exact filter: a candidate can
+// beat the k-th only if score >= k-th score, and the owners compare the exact
+// (score, index) key.  The MFMAs of block c+1 are issued before block c's filter
+// (two accumulator sets).
+// Early exit: V is swept by decreasing norm, so no later row has a norm above the
+// current tile's first row x 2^(1/128) (one bucket); a row whose k-th score
+// exceeds (|q| + 1)(that bound + 1)(1 + 2^-7) can gain nothing from the rest of
+// the sweep.  A wave whose rows are all there skips its tiles, and the workgroup
+// leaves the sweep when its four waves are.
 // Lists (TOPR > 0, top <= TOPR): each row's list lives in the registers of one
 // "owner" lane (lane 16g + rho owns row rho of group g), sorted by ascending
 // goodness with the k-th best at [0] (entries top..TOPR-1 are sentinels that
@@ -437,13 +476,15 @@ __device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
 }
 
 // MODE (dev ablation only, tools/dev_topk.hip; the product launches MODE 0):
-// 1 = scores only (no filter), 2 = filter against an unbeatable threshold (no
-// insertions), 3 = as 0 but each wave writes its count of exact-insertion calls
-// to score_out[wave] instead of the lists.
+// 1 = exact scores only (no filter), 2 = coarse filter against an unbeatable
+// threshold (no refinement, no insertions, no early exit), 3 = as 0 but each wave
+// writes its count of blocks past the coarse filter to score_out[wave] and of
+// tiles swept to score_out[4 grid + wave] instead of the lists.
 template <int NK, int RG, int TOPR, int MODE = 0>
 __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
                                                          const int32_t* __restrict__ perm,
+                                                         const float* __restrict__ vnorm,
                                                          int64_t n_v, int ld, int k, int top,
                                                          const float* __restrict__ scal,
                                                          int32_t* __restrict__ idx_out,
@@ -458,9 +499,12 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   extern __shared__ uint4 smem_u4[];
   uint4* tiles = smem_u4;                                     // [2][VT][RS]
   int* tperm = reinterpret_cast<int*>(tiles + 2 * VT * RS);   // [2][VT] V row of each tile row
+  int* sdone = tperm + 2 * VT;                                // [2][4] wave done flags
+  float* sqs = reinterpret_cast<float*>(sdone + 8);           // [4][RG][16] slack coefficients
   // TOPR == 0: [64 RG rows][top] keys (best first), [64 RG] lengths
-  // TOPR > 0: per wave and group a 16 x 16 score block [item m][row]
-  uint64_t* lk = reinterpret_cast<uint64_t*>(tperm + 2 * VT);  // 8-byte aligned: VT % 16 == 0
+  // TOPR > 0: per wave and group a 16 x 16 score block [item m][row], then per wave
+  // and group the rows' k-th scores
+  uint64_t* lk = reinterpret_cast<uint64_t*>(sqs + 64 * RG);  // 8-byte aligned: VT % 16 == 0
   int* len = reinterpret_cast<int*>(lk + 64 * RG * top);
   float* sblk = reinterpret_cast<float*>(lk);
 
@@ -481,6 +525,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     const int64_t row = qbase + 64 * g + 16 * w + m;
     const bool ok = row < n_q;
     bool nz = false;
+    float ss = 0.f;
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
 #pragma unroll
@@ -488,6 +533,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
         const int d = 32 * s + 8 * q + j;
         const float t = (ok && d < k) ? su * Q[row * ld + d] : 0.f;
         nz = nz || t != 0.f;
+        ss = fmaf(t, t, ss);
         _Float16 h, l;
         tk_split(t, h, l);
         ah[g][s][j] = h;
@@ -496,11 +542,19 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     }
     const uint64_t b = __ballot(nz);
     live[g] = (unsigned)((b | (b >> 16) | (b >> 32) | (b >> 48)) & 0xFFFFu);
+    ss += __shfl_xor(ss, 16);
+    ss += __shfl_xor(ss, 32);
+    // coarse-filter slack coefficient of row m, 2^-9 (|q| + 1): read from LDS once
+    // per tile and after insertions
+    if (q == 0) sqs[(w * RG + g) * 16 + m] = 0x1p-9f * (sqrtf(ss) + 1.f);
   }
   if (TOPR == 0 && threadIdx.x < 64 * RG) len[threadIdx.x] = 0;
+  // TOPR > 0: ts = the row's coarse threshold, k-th score - 2^-9 (|q| + 1)(NV + 1), NV
+  // bounding |v| from the current tile on (the k-th scores live in LDS, thr);
+  // TOPR == 0: (ts, ti) = the row's k-th (score, index).  Dead rows (absent or all
+  // zero) keep an unbeatable threshold.
   float ts[RG][4];
   int ti[RG][4];
-  // dead rows (absent or all-zero) keep an unbeatable threshold
 #pragma unroll
   for (int g = 0; g < RG; ++g)
 #pragma unroll
@@ -508,6 +562,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? -__builtin_inff() : __builtin_inff();
       ti[g][r] = 0x7fffffff;
     }
+  float* thr = sblk + 4 * RG * 256 + w * RG * 16;  // TOPR > 0: [g][row] k-th scores
+  if (TOPR > 0 && lane < 16 * RG)
+    thr[lane] = ((live[lane >> 4] >> (lane & 15)) & 1u) ? -__builtin_inff() : __builtin_inff();
   bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
   // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
   // sub-list of row m (every lane: sub-list q)
@@ -522,6 +579,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
 
   uint4 pre[PER];
   int pre_p = 0x7fffffff;
+  // norm of the first row of the fetched / current tile: V is sorted by decreasing
+  // norm, so x 2^(1/128) (one bucket) it bounds every row from that tile on
+  float nv_pre = 0.f, nv_cur = 0.f;
   auto fetch = [&](int64_t vb) {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
@@ -532,6 +592,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
                           : make_uint4(0x7E007E00u, 0x7E007E00u, 0x7E007E00u, 0x7E007E00u);
     }
     if (threadIdx.x < VT) pre_p = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
+    nv_pre = vnorm[vb];
   };
   auto stage = [&](int buf) {
     uint4* t = tiles + buf * VT * RS;
@@ -541,37 +602,63 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       t[(x / RW) * RS + x % RW] = pre[e];
     }
     if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p;
+    nv_cur = nv_pre;
   };
-  auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {
-    // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m
+  // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m
+  auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {  // hi.hi
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NK; ++s) {
+      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
+    }
+  };
+  auto refine = [&](const uint4* tb, floatx4 (&acc)[RG]) {  // + hi.lo + lo.hi
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
       const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
       const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[KQ / 8 + 4 * s + q]);
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bl, acc[g], 0, 0, 0);
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[g][s], bh, acc[g], 0, 0, 0);
       }
     }
   };
+  // (|q| + 1)-free part of the slack bound: NV + 1 for the current tile
+  float nvt = 1.f;
+  // TOPR > 0: coarse thresholds from the k-th scores in thr
+  auto refresh = [&]() {
+#pragma unroll
+    for (int g = 0; g < RG; ++g) {
+      const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
+      const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? fmaf(-s4[r], nvt, t4[r]) : __builtin_inff();
+    }
+  };
   float sink = 0.f;
-  int n_offer = 0;
-  auto filter = [&](const floatx4 (&acc)[RG], int64_t ibase, const int* bperm) {
+  int n_offer = 0, n_tiles = 0;
+  // acc: hi.hi scores of the block (refined in place when it passes the coarse
+  // filter); tbr: the block's B rows in the tile
+  auto filter = [&](floatx4 (&acc)[RG], int64_t ibase, const int* bperm, const uint4* tbr) {
     // acc[g][r] = scaled score(row 64g + 16w + 4q + r, V row ibase + m)
     if constexpr (MODE == 1) {
+      refine(tbr, acc);
 #pragma unroll
       for (int g = 0; g < RG; ++g) sink += fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
       return;
     }
     if constexpr (TOPR > 0) {
-      // score >= the row's k-th score (a tie may still win on the index: the
-      // owner lanes decide with beats()); until the lists are full every block
-      // goes to the owners.  Rows past n_v score NaN: no test passes them and
-      // beats() rejects them.
+      // coarse: hi.hi >= the coarse threshold; then the exact scores go to the
+      // owners against the same threshold (a weaker test than the k-th score: the
+      // owner lanes compare exact (score, index) keys); until the lists are full
+      // every block goes to the owners.  Rows past n_v score NaN: no test passes
+      // them and the owners reject them.
       const bool fullw = __builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0;
       if (fullw) {
         bool c = false;
@@ -581,14 +668,14 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= (MODE == 2 ? 3.0e38f : ts[g][r]);
         if (__ballot(c) == 0) return;
       }
+      refine(tbr, acc);
       bool pr[RG][4];
 #pragma unroll
       for (int g = 0; g < RG; ++g)
 #pragma unroll
         for (int r = 0; r < 4; ++r) pr[g][r] = !fullw || acc[g][r] >= ts[g][r];
       if constexpr (MODE == 3) ++n_offer;
-      float* st = sblk + w * RG * 256;              // [g][item m][row]
-      float* thr = sblk + 4 * RG * 256 + w * RG * 16;  // [g][row] new k-th scores
+      float* st = sblk + w * RG * 256;  // [g][item m][row]
       uint64_t b[RG][4];
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
@@ -642,13 +729,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
         thr[lane] = kv[0] == kTkKeyOpen ? -__builtin_inff() : tk_key_score(kv[0]);
       }
       asm volatile("" ::: "memory");
-#pragma unroll
-      for (int g = 0; g < RG; ++g) {
-        const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? t4[r] : __builtin_inff();
-      }
+      refresh();
       if (!full) {
         const bool open_list =
             QUAD ? (((live[0] >> m) & 1u) && kv[0] == kTkKeyOpen)
@@ -658,6 +739,17 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       return;
     }
     const bool vin = ibase + m < n_v;
+    if (full) {
+      bool c = false;
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = c || (vin && acc[g][r] >= fmaf(-s4[r], nvt, ts[g][r]));
+      }
+      if (__ballot(c) == 0) return;
+    }
+    refine(tbr, acc);
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
       bool hit = !full;
@@ -686,26 +778,57 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   int buf = 0;
   for (int64_t vb = 0; vb < n_v; vb += VT) {
     const uint4* tb = tiles + buf * VT * RS;
-    floatx4 acc0[RG], acc1[RG];
-    score(tb + m * RS, acc0);
+    nvt = fmaf(nv_cur, 1.01f, 1.f);
+    // early exit: every row of the wave holds a k-th score that no row from this
+    // tile on can reach: k-th > (|q| + 1)(NV + 1)(1 + 2^-7) (dead rows: +inf)
+    bool open = false;
+    if constexpr (TOPR > 0) {
+      if (MODE != 1) refresh();
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      // issue block c+1's MFMAs, then filter block c
-      if (c % 2 == 0) {
-        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc1);
-        filter(acc0, vb + 16 * c, tperm + buf * VT + 16 * c);
-      } else {
-        if (c + 1 < NC) score(tb + (16 * (c + 1) + m) * RS, acc0);
-        filter(acc1, vb + 16 * c, tperm + buf * VT + 16 * c);
+      for (int g = 0; g < RG; ++g) {
+        const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
+        const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          open = open || (((live[g] >> (4 * q + r)) & 1u) && !(t4[r] > (0x1p9f + 4.f) * s4[r] * nvt));
+      }
+    } else {
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) open = open || !(ts[g][r] > (0x1p9f + 4.f) * s4[r] * nvt);
+      }
+    }
+    const bool wdone = (MODE == 0 || MODE == 3) && __ballot(open) == 0;
+    if (!wdone) {
+      if constexpr (MODE == 3) ++n_tiles;
+      floatx4 acc0[RG], acc1[RG];
+      score(tb + m * RS, acc0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint4* tbr = tb + (16 * c + m) * RS;
+        // issue block c+1's MFMAs, then filter block c
+        if (c % 2 == 0) {
+          if (c + 1 < NC) score(tbr + 16 * RS, acc1);
+          filter(acc0, vb + 16 * c, tperm + buf * VT + 16 * c, tbr);
+        } else {
+          if (c + 1 < NC) score(tbr + 16 * RS, acc0);
+          filter(acc1, vb + 16 * c, tperm + buf * VT + 16 * c, tbr);
+        }
       }
     }
     if (vb + VT < n_v) stage(buf ^ 1);
+    if (lane == 0) sdone[buf * 4 + w] = wdone ? 1 : 0;
     __syncthreads();
+    // (flags of this buffer are rewritten only after the next barrier)
+    if (sdone[buf * 4] & sdone[buf * 4 + 1] & sdone[buf * 4 + 2] & sdone[buf * 4 + 3]) break;
     if (vb + 2 * VT < n_v) fetch(vb + 2 * VT);
     buf ^= 1;
   }
   if constexpr (MODE != 0) {
     if (lane == 0) score_out[blockIdx.x * 4 + w] = MODE == 1 ? sink : (float)n_offer;
+    if (MODE == 3 && lane == 0) score_out[(gridDim.x + blockIdx.x) * 4 + w] = (float)n_tiles;
     return;
   }
   if constexpr (QUAD) {
@@ -813,7 +936,10 @@ static bool topk_quad(int top, int64_t n_v) {
 static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
   const size_t vt = (size_t)tk_vt_q(nk, quad);
-  const size_t tiles = 16 * 2 * vt * (size_t)(kq / 4 + 2) + 4 * 2 * vt;
+  // [2][vt] tile rows of KQ hi + KQ lo halves (stride kq/4 + 2 uint4) | [2][vt] V rows |
+  // [2][4] done flags | [4][rg][16] slack coefficients
+  const size_t tiles =
+      16 * 2 * vt * (size_t)(kq / 4 + 2) + 4 * 2 * vt + 4 * 8 + 4 * 64 * (size_t)rg;
   if (top <= kTopR || quad) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
   return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
@@ -847,8 +973,9 @@ size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top
   (void)n_q;
   (void)top;
   // 256 B of scale words | split planes of V in sweep order (2 x KQ halves per row) |
-  // sweep order (int32 per V row) | bucket counts / cursors
-  return 256 + tk_table_bytes(n_v, k) + align_up(4 * (size_t)(n_v > 0 ? n_v : 0)) +
+  // sweep order (int32 per V row) | bucket counts / cursors | scaled row norms in
+  // sweep order (fp32 per V row)
+  return 256 + tk_table_bytes(n_v, k) + 2 * align_up(4 * (size_t)(n_v > 0 ? n_v : 0)) +
          align_up(4 * (size_t)kTkBuckets);
 }
 
@@ -878,6 +1005,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   _Float16* vsp = reinterpret_cast<_Float16*>(static_cast<char*>(ws) + 256);
   int32_t* perm = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + 256 + tk_table_bytes(n_v, k));
   int32_t* hist = perm + align_up(4 * (size_t)n_v) / 4;
+  float* vnorm = reinterpret_cast<float*>(hist + align_up(4 * (size_t)kTkBuckets) / 4);
   const int kq = topk_kq(k);
   const int kq_shift = __builtin_ctz(kq);
   ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
@@ -902,6 +1030,9 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     topk_split_table_kernel<<<(int)std::min<int64_t>(4096, (total + 255) / 256), 256, 0, st>>>(
         V, n_v, ld, k, kq_shift, scal, perm, vsp);
     ALS_LAUNCH_CHECK();
+    tk_table_norm_kernel<<<(int)std::min<int64_t>(4096, (n_v * 16 + 255) / 256), 256, 0, st>>>(
+        V, n_v, ld, k, scal, perm, vnorm);
+    ALS_LAUNCH_CHECK();
   }
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
   const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
@@ -910,8 +1041,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   do {                                                                                          \
     ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, TR>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
-    topk_split_kernel<NK, RG, TR><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld, k, top,  \
-                                                          scal, idx_out, score_out);            \
+    topk_split_kernel<NK, RG, TR><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld, k, \
+                                                          top, scal, idx_out, score_out);       \
     ALS_LAUNCH_CHECK();                                                                         \
   } while (0)
 #define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                 \

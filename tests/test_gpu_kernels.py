@@ -518,3 +518,90 @@ def test_topk_fewer_items_than_top(n_v, top):
     assert np.all(np.sort(idx[:, :n_v], axis=1) == np.arange(n_v))
     ref_i, ref_s = O.topk(Q.cpu().numpy(), Vm.cpu().numpy(), n_v)
     np.testing.assert_allclose(sc[:, :n_v], ref_s, rtol=1e-5, atol=1e-5)
+
+
+def _topk_check(Q, Vm, idx, sc, top, tol=1e-5):
+    """idx/sc vs the fp64 oracle: identical except where fp64 scores tie within tol."""
+    ref_i, ref_s = O.topk(Q, Vm, top)
+    S = Q.astype(np.float64) @ Vm.astype(np.float64).T
+    for row in range(Q.shape[0]):
+        if not np.array_equal(idx[row], ref_i[row]):
+            bad = np.nonzero(idx[row] != ref_i[row])[0]
+            for p_ in bad:
+                assert abs(S[row, idx[row, p_]] - ref_s[row, p_]) <= tol * max(1, abs(ref_s[row, p_])), \
+                    (row, p_, idx[row, p_], ref_i[row, p_])
+        np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
+    return ref_i, ref_s
+
+
+def _topk_dev(Q, Vm, rank, top):
+    ld = E.ld_for(rank)
+    Qd = torch.zeros((Q.shape[0], ld), device=DEV)
+    Qd[:, :rank] = torch.as_tensor(Q).to(DEV)
+    Vd = torch.zeros((Vm.shape[0], ld), device=DEV)
+    Vd[:, :rank] = torch.as_tensor(Vm).to(DEV)
+    idx, sc = E.topk_rows(Qd, Q.shape[0], Vd, Vm.shape[0], rank, top)
+    return idx.cpu().numpy(), sc.cpu().numpy()
+
+
+@pytest.mark.parametrize("rank,top", [(64, 10), (128, 10), (128, 100), (32, 40), (128, 200)])
+def test_topk_scores_finer_than_f16(rank, top):
+    """The coarse filter scores hi.hi only (f16 rounding ~5e-4 relative): V rows that
+    differ from one strong row by relative steps of 4e-5 (below the f16 resolution of
+    every element, above the 1e-5 tie tolerance) must still be ranked by their exact
+    fp32-grade scores, i.e. the refinement decides every near-threshold pair."""
+    rng = np.random.default_rng(rank * 7 + top)
+    n_q, n_v = 128, 6000
+    Q = rng.standard_normal((n_q, rank)).astype(np.float32)
+    Vm = rng.standard_normal((n_v, rank)).astype(np.float32)
+    base = rng.standard_normal(rank).astype(np.float32) * 3.0
+    fam = rng.permutation(n_v)[:400]  # a family of near-copies scattered over the index range
+    steps = (1.0 + 4e-5 * rng.integers(-60, 60, fam.size)).astype(np.float32)
+    Vm[fam] = base[None, :] * steps[:, None]
+    Q[: n_q // 2] = np.abs(Q[: n_q // 2]) * np.sign(base)[None, :]  # half the rows favour the family
+    idx, sc = _topk_dev(Q, Vm, rank, top)
+    ref_i, _ = _topk_check(Q, Vm, idx, sc, top)
+    assert np.isin(ref_i[: n_q // 2], fam).mean() > 0.5  # the family dominates those lists
+
+
+@pytest.mark.parametrize("rank,top", [(64, 10), (128, 16), (128, 100), (64, 150)])
+def test_topk_wide_norm_spread_early_exit(rank, top):
+    """V norms spread over six decades (most rows tiny): the norm-ordered sweep lets a
+    workgroup stop once no remaining row can reach its rows' k-th scores; query rows of
+    very different norms share a wavefront; results must equal the full sweep's."""
+    rng = np.random.default_rng(rank + 3 * top)
+    n_q, n_v = 200, 40000
+    Q = (rng.standard_normal((n_q, rank)) * 10.0 ** rng.uniform(-3, 3, (n_q, 1))).astype(np.float32)
+    Vm = (rng.standard_normal((n_v, rank)) * 10.0 ** rng.uniform(-6, 0, (n_v, 1))).astype(np.float32)
+    Vm[rng.permutation(n_v)[:300]] *= 50.0  # a few strong rows
+    Q[17] = 0.0
+    idx, sc = _topk_dev(Q, Vm, rank, top)
+    _topk_check(Q, Vm, idx, sc, top)
+    assert list(idx[17]) == list(range(top))
+
+
+@pytest.mark.parametrize("rank,top", [(64, 10), (128, 100), (64, 200)])
+def test_topk_nan_factor_row(rank, top):
+    """A V row holding a NaN (e.g. a loaded model) scores NaN: it is never listed, and
+    every other row ranks as if it were absent."""
+    rng = np.random.default_rng(rank + top + 11)
+    n_q, n_v = 150, 3000
+    Q = rng.standard_normal((n_q, rank)).astype(np.float32)
+    Vm = rng.standard_normal((n_v, rank)).astype(np.float32)
+    Vm *= rng.uniform(0.2, 2.0, (n_v, 1)).astype(np.float32)
+    bad = [5, 1234]
+    Vm[5, 3] = np.nan
+    Vm[1234, 0] = np.nan
+    idx, sc = _topk_dev(Q, Vm, rank, top)
+    assert not np.isin(idx, bad).any()
+    keep = np.setdiff1d(np.arange(n_v), bad)
+    ref_i, ref_s = O.topk(Q, Vm[keep], top)
+    ref_i = keep[ref_i]
+    S = Q.astype(np.float64) @ Vm[keep].astype(np.float64).T
+    for row in range(n_q):
+        if not np.array_equal(idx[row], ref_i[row]):
+            for p_ in np.nonzero(idx[row] != ref_i[row])[0]:
+                assert abs(Q[row].astype(np.float64) @ Vm[idx[row, p_]].astype(np.float64)
+                           - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
+        np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
+    del S

@@ -1,19 +1,14 @@
 #!/bin/bash
 # Dev A/B of top-k kernel variants (NOT product code): each variant's topk.hip is
 # compiled into its own tools/ab/libtk_<tag>.so exposing ab_topk() = its als_topk.
-#   v0 = round-2 kernel (register staging, quad lists with one row group)
-#   v1 = bf088e3 (register staging, quad lists with two row groups)
-#   v2 = HEAD (LDS-DMA staging, quad two row groups)
-#   v3 = HEAD with one row group for quad lists
+#   base = the committed kernel (git HEAD, or the revision given as $1)
+#   new  = the working-tree kernel
 set -e
 cd "$(dirname "$0")"
 CSRC=../../recommender-system-using-apache-spark-mllib-_amd/csrc
-git show ad16911:recommender-system-using-apache-spark-mllib-_amd/csrc/topk.hip > tk_v0.hip
-git show bf088e3:recommender-system-using-apache-spark-mllib-_amd/csrc/topk.hip > tk_v1.hip
-cp $CSRC/topk.hip tk_v2.hip
-sed 's|  if (quad) return 2;  // quad lists: two row groups (each V tile feeds 128 query rows)|  if (quad) return 1;|' $CSRC/topk.hip > tk_v3.hip
-grep -q "if (quad) return 1;" tk_v3.hip
-for v in v0 v1 v2 v3; do
+git show ${1:-HEAD}:recommender-system-using-apache-spark-mllib-_amd/csrc/topk.hip > tk_base.hip
+cp $CSRC/topk.hip tk_new.hip
+for v in base new; do
   cat > ab_$v.hip <<EOT
 #include "tk_$v.hip"
 namespace als { void set_error(const char*, ...) {} }

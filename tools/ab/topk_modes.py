@@ -38,7 +38,7 @@ def main():
                          dtype=torch.uint8, device=dev)
         idx = torch.empty((s, top), dtype=torch.int32, device=dev)
         sc = torch.empty((s, top), dtype=torch.float32, device=dev)
-        dbg = torch.zeros(s * 4 + 64, dtype=torch.float32, device=dev)
+        dbg = torch.zeros(s * 8 + 64, dtype=torch.float32, device=dev)
         st = torch.cuda.current_stream().cuda_stream
         for mode in (0, 1, 2, 3, 0):
             args = (mode, Q.data_ptr(), s, core.V.data_ptr(), n_v, Q.shape[1], 128, top,
@@ -55,7 +55,12 @@ def main():
                 rg = 2 if top <= 16 else 1
                 waves = (s + 64 * rg - 1) // (64 * rg) * 4
                 cnt = dbg[:waves].double()
-                extra = f" offers/wave mean {float(cnt.mean()):.0f} of {(n_v + 15) // 16 * rg} blocks"
+                til = dbg[waves:2 * waves].double()
+                vt = 64 // 4 * (4 if top > 16 else 1)
+                extra = (f" refined blocks/wave mean {float(cnt.mean()):.0f} of "
+                         f"{(n_v + 15) // 16} blocks; tiles/wave mean {float(til.mean()):.0f} "
+                         f"min {float(til.min()):.0f} max {float(til.max()):.0f} of "
+                         f"{(n_v + vt - 1) // vt}")
             print(f"top{top} mode {mode}: {e0.elapsed_time(e1):.1f} ms{extra}", flush=True)
 
 

@@ -24,22 +24,24 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
   const uint4* vsp4 = reinterpret_cast<const uint4*>(static_cast<char*>(ws) + 256);
   const int32_t* perm =
       reinterpret_cast<const int32_t*>(static_cast<char*>(ws) + 256 + tk_table_bytes(n_v, k));
+  const float* vnorm = reinterpret_cast<const float*>(
+      perm + align_up(4 * (size_t)n_v) / 4 + align_up(4 * (size_t)kTkBuckets) / 4);
 #define L(NK, RG, M)                                                                          \
   do {                                                                                        \
     if (top <= kTopR) { /* the product picks 8 / 12 / 16 by top: the dev modes use 16 */    \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, kTopR, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,  \
+      topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld,  \
                                                                   k, top, scal, idx, dbg);    \
     } else if (quad) { /* quad lists (rg is 1 here): the dev modes use 100 (configs[4]) */   \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, 1, 100, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, 1, 100, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld,   \
+      topk_split_kernel<NK, 1, 100, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld,   \
                                                                k, top, scal, idx, dbg);       \
     } else {                                                                                  \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, 0, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, 0, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, n_v, ld, k, \
+      topk_split_kernel<NK, RG, 0, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld, k, \
                                                               top, scal, idx, dbg);           \
     }                                                                                         \
   } while (0)

@@ -1,0 +1,42 @@
+"""Dev: per-kernel register / occupancy / spill table of one HIP source (gfx950),
+from clang's kernel-resource-usage remarks.
+    python tools/regs.py path/to/file.hip [name-filter]"""
+import re
+import subprocess
+import sys
+
+
+def main():
+    src = sys.argv[1]
+    filt = sys.argv[2] if len(sys.argv) > 2 else ""
+    inc = "-I" + src.rsplit("/", 1)[0] if "/" in src else "-I."
+    p = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", inc,
+                        "-c", src, "-o", "/tmp/_regs.o", "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True)
+    cur = None
+    rows = []
+    for line in p.stderr.splitlines():
+        m = re.search(r"remark: \s*(.*?): (.*?) \[-Rpass", line)
+        if not m:
+            continue
+        key, val = m.group(1), m.group(2)
+        if key == "Function Name":
+            cur = {"name": val}
+            rows.append(cur)
+        elif cur is not None:
+            cur[key] = val
+    if p.returncode != 0:
+        print(p.stderr[-3000:])
+    for r in rows:
+        if filt and filt not in r["name"]:
+            continue
+        dm = subprocess.run(["c++filt", r["name"]], capture_output=True,
+                            text=True).stdout.strip()
+        dm = re.sub(r"\(.*\)$", "", dm)
+        print(f"{dm[:70]:70s} V{r.get('VGPRs', '?'):>4} A{r.get('AGPRs', '?'):>3} "
+              f"occ {r.get('Occupancy [waves/SIMD]', '?')} vspill {r.get('VGPRs Spill', '?')} "
+              f"sspill {r.get('SGPRs Spill', '?')}")
+
+
+if __name__ == "__main__":
+    main()

@@ -350,8 +350,8 @@ __global__ __launch_bounds__(256) void tk_table_norm_kernel(const float* __restr
   }
 }
 
-// V -> split planes in sweep order, table row t = V row perm[t]:
-// [hi(sv v[0..KQ)) | lo(sv v[0..KQ))] (f16), dims >= k zero.
+// V -> split planes in sweep order, table row t = V row perm[t]: hi plane
+// [n_v][KQ] = hi(sv v), then lo plane [n_v][KQ] = lo(sv v) (f16), dims >= k zero.
 __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __restrict__ V,
                                                                int64_t n_v, int ld, int k,
                                                                int kq_shift,
@@ -368,36 +368,46 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
     const float t = d < k ? sv * V[(int64_t)perm[r] * ld + d] : 0.f;
     _Float16 h, l;
     tk_split(t, h, l);
-    out[2 * (r << kq_shift) + d] = h;
-    out[2 * (r << kq_shift) + kq + d] = l;
+    out[e] = h;
+    out[total + e] = l;
   }
 }
 
 // Split-f16 scores.  NK = KQ / 32 MFMA k-steps (KQ = k padded to 32, 64 or 128);
-// RG query-row groups of 64 per workgroup.  scal[0] = max |Q|, scal[1] = max |V|.
+// RG query-row groups of 16 NW rows per workgroup (NW wavefronts, tk_nw).
+// scal[0] = max |Q|, scal[1] = max |V|.
 //
-// V is swept in tiles of kTkVT(NK) rows, double-buffered in LDS: tile t+1 is
-// written (from registers loaded one tile earlier) while nothing reads its
-// buffer, so ONE barrier per tile; the global loads of tile t+2 are then in
-// flight during tile t+1's MFMAs.  LDS rows are RW + 2 uint4 apart: the
-// ds_read_b128 lane groups of gfx950 ({0-3,12-15,20-27}, ...) then touch 16
-// distinct 4-bank slots (row stride = 2 mod 16 slots), conflict-free.
+// The sweep is bound by how many V bytes are in flight from L2 / HBM, not by the
+// matrix cores (dev ablation at configs[4]: the hi.hi sweep alone ran at ~4.5 TB/s
+// with 8-16 KB of tile loads in flight per workgroup, i.e. one L2-miss latency per
+// tile), so the design minimises the V bytes streamed per query row:
+//  * only the hi plane of V is staged (256 B per row at KQ = 128, half the split
+//    table); the lo halves are fetched for the rare refined blocks;
+//  * with register lists a workgroup is 8 wavefronts (128 RG query rows per tile
+//    stream; one workgroup per CU at the lists' register count) and a tile is 16-32
+//    KB, so each L2 latency delivers more rows.
+// Tiles are double-buffered in LDS: tile t+1 is written (from registers loaded one
+// tile earlier) while nothing reads its buffer, so ONE barrier per tile; the global
+// loads of tile t+2 are in flight during tile t+1's MFMAs.  LDS rows are RW + 2
+// uint4 apart (RW = 4 NK): the ds_read_b128 lane groups of gfx950
+// ({0-3,12-15,20-27}, ...) then touch 16 distinct 4-bank slots (row stride = 2 x odd
+// mod 16 slots), conflict-free.
 // Coarse filter, exact refinement: a block is first scored with hi.hi alone (one
 // MFMA per k-step instead of three).  The dropped terms hi.lo + lo.hi are bounded
 // by 2^-10 |q| |v| (Cauchy-Schwarz on |lo| <= 2^-11 |t|, plus the f16 subnormal
 // and fp32 accumulation terms, all far below it), so a pair can reach its row's
-// k-th score only if hi.hi >= k-th - 2^-9 (|q| + 1)(|v| + 1): one fma and one
-// compare per score, one ballot per 16 x 16 block.  A block with a pair past that
-// bound gets the hi.lo + lo.hi MFMAs added (the exact score every pair is ranked
-// by, the same wherever the pair is met), then the exact filter: a candidate can
-// beat the k-th only if score >= k-th score, and the owners compare the exact
-// (score, index) key.  The MFMAs of block c+1 are issued before block c's filter
-// (two accumulator sets).
+// k-th score only if hi.hi >= k-th - 2^-9 (|q| + 1)(NV + 1), NV >= |v| for every row
+// from the current tile on: one compare per score, one ballot per 16 x 16 block.  A
+// block with a pair past that bound gets its lo halves by LDS-DMA and the hi.lo +
+// lo.hi MFMAs added (the exact score every pair is ranked by, the same wherever
+// the pair is met); the owners then compare the exact (score, index) keys.  The
+// MFMAs of block c+1 are issued before block c's filter (two accumulator sets).
 // Early exit: V is swept by decreasing norm, so no later row has a norm above the
 // current tile's first row x 2^(1/128) (one bucket); a row whose k-th score
 // exceeds (|q| + 1)(that bound + 1)(1 + 2^-7) can gain nothing from the rest of
 // the sweep.  A wave whose rows are all there skips its tiles, and the workgroup
-// leaves the sweep when its four waves are.
+// leaves the sweep when all its waves are (at configs[4] the factor norms are too
+// concentrated for this to trigger; it pays on long-tailed norm spreads).
 // Lists (TOPR > 0, top <= TOPR): each row's list lives in the registers of one
 // "owner" lane (lane 16g + rho owns row rho of group g), sorted by ascending
 // goodness with the k-th best at [0] (entries top..TOPR-1 are sentinels that
@@ -405,26 +415,22 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // branch-free bubble pass.  A block with survivors stages its 16 x 16 scores in
 // LDS (one ds_write_b128 per lane); each owner lane takes its row's survivors
 // from the ballots, inserts them, and the new k-th scores go back to the
-// filtering lanes by ds_bpermute.  16 < top <= 128 (TOPR = 32 / 64 / 128, one row
-// group): quad lists — a row's list is split over its four lanes 16j + rho as
+// filtering lanes through LDS.  16 < top <= 128 (TOPR = 32 / 64 / 100 / 128, one
+// row group): quad lists — a row's list is split over its four lanes 16j + rho as
 // sorted sub-lists of TOPR / 4 keys; the row's k-th best is the least of their
 // four minima (two lane swaps), an insertion replaces that minimum in the lane
 // holding it, and every row of the wave inserts in the same pass (the LDS path
 // below inserts one candidate per wave at a time: 70 ms vs 13.6 ms of scores at
 // rank 128 top 100 on the ML-25M shape).  The output ranks each entry by counting
-// the larger keys of the four sub-lists; its tiles are 4x taller (tk_vt_q).
+// the larger keys of the four sub-lists.
 // TOPR = 0 (top > 128): sorted lists in LDS, wave-cooperative insertion
-// (topk_offer).
-// Tile rows: 64 / NK keeps the staging registers at 2 x uint4 per thread; larger
-// tiles cost occupancy (measured: 128 / NK and 192 / NK slower on ML-25M shapes).
-__host__ __device__ constexpr int tk_vt(int nk) { return 64 / nk; }
-// Quad lists: 4x taller tiles (2x at NK = 1, to keep two workgroups per CU).  The
-// workgroup's barrier per tile couples its waves, so one wave's (rare, long)
-// insertion pass stalls the other three; fewer barriers spread that cost, and the
-// quad kernel is register-bound at two workgroups per CU anyway, which leaves LDS
-// for the taller tiles (measured, configs[4] top-100: 1x 584 ms, 2x 397, 4x 330).
-__host__ __device__ constexpr int tk_vt_q(int nk, bool quad) {
-  return quad ? (nk == 1 ? 2 : 4) * tk_vt(nk) : tk_vt(nk);
+// (topk_offer), 4 wavefronts.
+// Tile rows (hi halves only, RW = 4 NK uint4 per row): register lists (8
+// wavefronts) 128 rows at NK = 4 (4 staged uint4 per thread), 256 / NK below (2 per
+// thread); LDS lists (4 wavefronts) 64 / NK rows (1 per thread), which leaves the
+// LDS to the lists.
+__host__ __device__ constexpr int tk_vt(int nk, int topr) {
+  return topr == 0 ? 64 / nk : (nk == 4 ? 128 : 256 / nk);
 }
 
 // Insert key `c` into a list sorted ascending (the k-th best at [0]; sentinels past
@@ -479,42 +485,50 @@ __device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
 // 1 = exact scores only (no filter), 2 = coarse filter against an unbeatable
 // threshold (no refinement, no insertions, no early exit), 3 = as 0 but each wave
 // writes its count of blocks past the coarse filter to score_out[wave] and of
-// tiles swept to score_out[4 grid + wave] instead of the lists.
+// tiles swept to score_out[waves + wave] instead of the lists.
+// Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
+// rows), 4 with LDS lists (top > 128: the lists of 64 RG rows fill the LDS).
+__host__ __device__ constexpr int tk_nw(int topr) { return topr > 0 ? 8 : 4; }
 template <int NK, int RG, int TOPR, int MODE = 0>
-__global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
+__global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
+                                                         const uint4* __restrict__ Vlo,
                                                          const int32_t* __restrict__ perm,
                                                          const float* __restrict__ vnorm,
                                                          int64_t n_v, int ld, int k, int top,
                                                          const float* __restrict__ scal,
                                                          int32_t* __restrict__ idx_out,
                                                          float* __restrict__ score_out) {
+  constexpr int NW = tk_nw(TOPR);      // wavefronts
+  constexpr int NT = 64 * NW;          // threads
+  constexpr int GR = 16 * NW;          // query rows of a row group
   constexpr int KQ = 32 * NK;
-  constexpr int RW = KQ / 4;           // uint4 per split row (KQ hi + KQ lo halves)
+  constexpr int RW = KQ / 8;           // uint4 per row of a split plane (KQ halves)
   constexpr int RS = RW + 2;           // LDS row stride in uint4 (bank-conflict-free)
-  constexpr int VT = tk_vt_q(NK, TOPR > 16);  // V rows per tile
+  constexpr int VT = tk_vt(NK, TOPR);  // V rows per tile
   constexpr int NC = VT / 16;          // 16-row score blocks per tile
-  constexpr int PER = VT * RW / 256;   // staged uint4 per thread per tile
-  static_assert(PER * 256 == VT * RW, "tile staging");
+  constexpr int PER = VT * RW / NT;    // staged uint4 per thread per tile
+  static_assert(PER * NT == VT * RW && VT <= NT, "tile staging");
   extern __shared__ uint4 smem_u4[];
   uint4* tiles = smem_u4;                                     // [2][VT][RS]
   int* tperm = reinterpret_cast<int*>(tiles + 2 * VT * RS);   // [2][VT] V row of each tile row
-  int* sdone = tperm + 2 * VT;                                // [2][4] wave done flags
-  float* sqs = reinterpret_cast<float*>(sdone + 8);           // [4][RG][16] slack coefficients
-  // TOPR == 0: [64 RG rows][top] keys (best first), [64 RG] lengths
+  int* sdone = tperm + 2 * VT;                                // [2][NW] wave done flags
+  float* sqs = reinterpret_cast<float*>(sdone + 2 * NW);      // [NW][RG][16] slack coefficients
+  uint4* loscr = reinterpret_cast<uint4*>(sqs + GR * RG);     // [NW][NK][64] lo of a refined block
+  // TOPR == 0: [GR RG rows][top] keys (best first), [GR RG] lengths
   // TOPR > 0: per wave and group a 16 x 16 score block [item m][row], then per wave
   // and group the rows' k-th scores
-  uint64_t* lk = reinterpret_cast<uint64_t*>(sqs + 64 * RG);  // 8-byte aligned: VT % 16 == 0
-  int* len = reinterpret_cast<int*>(lk + 64 * RG * top);
+  uint64_t* lk = reinterpret_cast<uint64_t*>(loscr + NW * NK * 64);  // 16-byte aligned
+  int* len = reinterpret_cast<int*>(lk + GR * RG * top);
   float* sblk = reinterpret_cast<float*>(lk);
 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
-  const int64_t qbase = (int64_t)blockIdx.x * 64 * RG;
+  const int64_t qbase = (int64_t)blockIdx.x * GR * RG;
   const int eu = tk_split_exponent(scal[0]), ev = tk_split_exponent(scal[1]);
   const float su = ldexpf(1.f, eu), unscale = ldexpf(1.f, -eu - ev);
 
   // A operands: group g, k-step s, lane (q, m): dims 32s + 8q .. +7 of query row
-  // qbase + 64g + 16w + m, as hi and lo halves.
+  // qbase + GR g + 16w + m, as hi and lo halves.
   tk_half8 ah[RG][NK], al[RG][NK];
   // live[g] bit rho: query row 16w + rho of group g exists and is not all zero (an
   // all-zero row scores 0 everywhere: its list is the first `top` rows, written at
@@ -522,7 +536,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   unsigned live[RG];
 #pragma unroll
   for (int g = 0; g < RG; ++g) {
-    const int64_t row = qbase + 64 * g + 16 * w + m;
+    const int64_t row = qbase + GR * g + 16 * w + m;
     const bool ok = row < n_q;
     bool nz = false;
     float ss = 0.f;
@@ -548,7 +562,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     // per tile and after insertions
     if (q == 0) sqs[(w * RG + g) * 16 + m] = 0x1p-9f * (sqrtf(ss) + 1.f);
   }
-  if (TOPR == 0 && threadIdx.x < 64 * RG) len[threadIdx.x] = 0;
+  if (TOPR == 0 && threadIdx.x < GR * RG) len[threadIdx.x] = 0;
   // TOPR > 0: ts = the row's coarse threshold, k-th score - 2^-9 (|q| + 1)(NV + 1), NV
   // bounding |v| from the current tile on (the k-th scores live in LDS, thr);
   // TOPR == 0: (ts, ti) = the row's k-th (score, index).  Dead rows (absent or all
@@ -562,7 +576,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? -__builtin_inff() : __builtin_inff();
       ti[g][r] = 0x7fffffff;
     }
-  float* thr = sblk + 4 * RG * 256 + w * RG * 16;  // TOPR > 0: [g][row] k-th scores
+  float* thr = sblk + NW * RG * 256 + w * RG * 16;  // TOPR > 0: [g][row] k-th scores
   if (TOPR > 0 && lane < 16 * RG)
     thr[lane] = ((live[lane >> 4] >> (lane & 15)) & 1u) ? -__builtin_inff() : __builtin_inff();
   bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
@@ -585,7 +599,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   auto fetch = [&](int64_t vb) {
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const int x = threadIdx.x + 256 * e;
+      const int x = threadIdx.x + NT * e;
       const int64_t vrow = vb + x / RW;
       // rows past n_v: f16 NaNs, so their scores are NaN and never pass a filter
       pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW]
@@ -598,7 +612,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     uint4* t = tiles + buf * VT * RS;
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const int x = threadIdx.x + 256 * e;
+      const int x = threadIdx.x + NT * e;
       t[(x / RW) * RS + x % RW] = pre[e];
     }
     if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p;
@@ -616,11 +630,20 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
     }
   };
-  auto refine = [&](const uint4* tb, floatx4 (&acc)[RG]) {  // + hi.lo + lo.hi
+  // + hi.lo + lo.hi.  The lo halves of the block's V rows come from the lo plane in
+  // global memory (only blocks past the coarse filter need them), by LDS-DMA into the
+  // wave's scratch: each lane reads back the 16 B it loaded, and no VGPR holds them.
+  auto refine = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG]) {
+    const int64_t vr = ibase + m < n_v ? ibase + m : n_v - 1;  // rows past n_v: NaN anyway
+    uint4* scr = loscr + w * NK * 64;
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+      __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
       const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
-      const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[KQ / 8 + 4 * s + q]);
+      const tk_half8 bl = __builtin_bit_cast(tk_half8, scr[s * 64 + lane]);
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bl, acc[g], 0, 0, 0);
@@ -646,9 +669,9 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   // acc: hi.hi scores of the block (refined in place when it passes the coarse
   // filter); tbr: the block's B rows in the tile
   auto filter = [&](floatx4 (&acc)[RG], int64_t ibase, const int* bperm, const uint4* tbr) {
-    // acc[g][r] = scaled score(row 64g + 16w + 4q + r, V row ibase + m)
+    // acc[g][r] = scaled score(row GR g + 16w + 4q + r, V row ibase + m)
     if constexpr (MODE == 1) {
-      refine(tbr, acc);
+      refine(tbr, ibase, acc);
 #pragma unroll
       for (int g = 0; g < RG; ++g) sink += fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
       return;
@@ -668,7 +691,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
           for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= (MODE == 2 ? 3.0e38f : ts[g][r]);
         if (__ballot(c) == 0) return;
       }
-      refine(tbr, acc);
+      refine(tbr, ibase, acc);
       bool pr[RG][4];
 #pragma unroll
       for (int g = 0; g < RG; ++g)
@@ -749,7 +772,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
       if (__ballot(c) == 0) return;
     }
-    refine(tbr, acc);
+    refine(tbr, ibase, acc);
 #pragma unroll
     for (int g = 0; g < RG; ++g) {
       bool hit = !full;
@@ -760,13 +783,13 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       }
       if constexpr (MODE == 3) n_offer += hit ? 1 : 0;
       if (hit)
-        topk_offer(acc[g], (int)ibase, n_v, bperm, ts[g], ti[g], lk, len, 64 * g + 16 * w,
+        topk_offer(acc[g], (int)ibase, n_v, bperm, ts[g], ti[g], lk, len, GR * g + 16 * w,
                    top, live[g]);
     }
     if (!full) {
       bool f = true;
       if (lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u))
-        f = len[64 * (lane >> 4) + 16 * w + (lane & 15)] >= top;
+        f = len[GR * (lane >> 4) + 16 * w + (lane & 15)] >= top;
       full = __ballot(!f) == 0;
     }
   };
@@ -805,30 +828,33 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
       if constexpr (MODE == 3) ++n_tiles;
       floatx4 acc0[RG], acc1[RG];
       score(tb + m * RS, acc0);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
+      // block pairs: issue block c+1's MFMAs, then filter block c
+#pragma unroll 1
+      for (int c = 0; c < NC; c += 2) {
         const uint4* tbr = tb + (16 * c + m) * RS;
-        // issue block c+1's MFMAs, then filter block c
-        if (c % 2 == 0) {
-          if (c + 1 < NC) score(tbr + 16 * RS, acc1);
-          filter(acc0, vb + 16 * c, tperm + buf * VT + 16 * c, tbr);
-        } else {
-          if (c + 1 < NC) score(tbr + 16 * RS, acc0);
-          filter(acc1, vb + 16 * c, tperm + buf * VT + 16 * c, tbr);
+        const int* bp = tperm + buf * VT + 16 * c;
+        if (NC > 1) score(tbr + 16 * RS, acc1);
+        filter(acc0, vb + 16 * c, bp, tbr);
+        if (NC > 1) {
+          if (c + 2 < NC) score(tbr + 32 * RS, acc0);
+          filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
         }
       }
     }
     if (vb + VT < n_v) stage(buf ^ 1);
-    if (lane == 0) sdone[buf * 4 + w] = wdone ? 1 : 0;
+    if (lane == 0) sdone[buf * NW + w] = wdone ? 1 : 0;
     __syncthreads();
     // (flags of this buffer are rewritten only after the next barrier)
-    if (sdone[buf * 4] & sdone[buf * 4 + 1] & sdone[buf * 4 + 2] & sdone[buf * 4 + 3]) break;
+    int alldone = 1;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) alldone &= sdone[buf * NW + i];
+    if (alldone) break;
     if (vb + 2 * VT < n_v) fetch(vb + 2 * VT);
     buf ^= 1;
   }
   if constexpr (MODE != 0) {
-    if (lane == 0) score_out[blockIdx.x * 4 + w] = MODE == 1 ? sink : (float)n_offer;
-    if (MODE == 3 && lane == 0) score_out[(gridDim.x + blockIdx.x) * 4 + w] = (float)n_tiles;
+    if (lane == 0) score_out[blockIdx.x * NW + w] = MODE == 1 ? sink : (float)n_offer;
+    if (MODE == 3 && lane == 0) score_out[(gridDim.x + blockIdx.x) * NW + w] = (float)n_tiles;
     return;
   }
   if constexpr (QUAD) {
@@ -894,7 +920,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
     return;
   } else if constexpr (TOPR > 0) {
     if (lane < 16 * RG) {
-      const int64_t row = qbase + 64 * (lane >> 4) + 16 * w + (lane & 15);
+      const int64_t row = qbase + GR * (lane >> 4) + 16 * w + (lane & 15);
       const bool zero = !((live[lane >> 4] >> (lane & 15)) & 1u);
       if (row < n_q) {
 #pragma unroll
@@ -917,7 +943,7 @@ __global__ __launch_bounds__(256) void topk_split_kernel(const float* __restrict
   }
 #pragma unroll
   for (int g = 0; g < RG; ++g)
-    topk_write(lk, len, 64 * g + 16 * w, qbase, n_q, n_v, top, unscale, live[g], idx_out,
+    topk_write(lk, len, GR * g + 16 * w, qbase, n_q, n_v, top, unscale, live[g], idx_out,
                score_out);
 }
 
@@ -935,12 +961,13 @@ static bool topk_quad(int top, int64_t n_v) {
 
 static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
-  const size_t vt = (size_t)tk_vt_q(nk, quad);
-  // [2][vt] tile rows of KQ hi + KQ lo halves (stride kq/4 + 2 uint4) | [2][vt] V rows |
-  // [2][4] done flags | [4][rg][16] slack coefficients
-  const size_t tiles =
-      16 * 2 * vt * (size_t)(kq / 4 + 2) + 4 * 2 * vt + 4 * 8 + 4 * 64 * (size_t)rg;
-  if (top <= kTopR || quad) return tiles + sizeof(float) * 4 * (size_t)rg * (256 + 16);
+  const int nw = (top <= kTopR || quad) ? 8 : 4;
+  const size_t vt = (size_t)tk_vt(nk, nw == 8 ? 1 : 0);
+  // [2][vt] tile rows of KQ hi halves (stride kq/8 + 2 uint4) | [2][vt] V rows |
+  // [2][4] done flags | [4][rg][16] slack coefficients | [4][nk][64] uint4 lo scratch
+  const size_t tiles = 16 * 2 * vt * (size_t)(kq / 8 + 2) + 4 * 2 * vt + 4 * 2 * nw +
+                       4 * 16 * nw * (size_t)rg + 16 * nw * 64 * (size_t)nk;
+  if (nw == 8) return tiles + sizeof(float) * nw * (size_t)rg * (256 + 16);
   return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
 }
@@ -1035,14 +1062,17 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     ALS_LAUNCH_CHECK();
   }
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
-  const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
+  const int nw = (top <= kTopR || quad) ? tk_nw(1) : tk_nw(0);  // wavefronts per workgroup
+  const unsigned grid = (unsigned)((n_q + 16 * nw * rg - 1) / (16 * nw * rg));
   const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
+  const uint4* vlo4 = vsp4 + n_v * (kq / 8);  // lo plane
 #define ALS_TOPK_SPLIT_LAUNCH2(NK, RG, TR)                                                      \
   do {                                                                                          \
     ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, TR>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
-    topk_split_kernel<NK, RG, TR><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld, k, \
-                                                          top, scal, idx_out, score_out);       \
+    topk_split_kernel<NK, RG, TR><<<grid, 64 * nw, lds, st>>>(Q, n_q, vsp4, vlo4, perm, vnorm,   \
+                                                          n_v, ld, k, top, scal, idx_out,       \
+                                                          score_out);                           \
     ALS_LAUNCH_CHECK();                                                                         \
   } while (0)
 #define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                 \

@@ -53,10 +53,10 @@ def main():
             extra = ""
             if mode == 3:
                 rg = 2 if top <= 16 else 1
-                waves = (s + 64 * rg - 1) // (64 * rg) * 4
+                waves = (s + 128 * rg - 1) // (128 * rg) * 8
                 cnt = dbg[:waves].double()
                 til = dbg[waves:2 * waves].double()
-                vt = 64 // 4 * (4 if top > 16 else 1)
+                vt = 128
                 extra = (f" refined blocks/wave mean {float(cnt.mean()):.0f} of "
                          f"{(n_v + 15) // 16} blocks; tiles/wave mean {float(til.mean()):.0f} "
                          f"min {float(til.min()):.0f} max {float(til.max()):.0f} of "

@@ -19,7 +19,8 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
   const int rg = topk_split_rg(k, top, quad);
   if (rg == 0) return -1;
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
-  const unsigned grid = (unsigned)((n_q + 64 * rg - 1) / (64 * rg));
+  const int nw = (top <= kTopR || quad) ? tk_nw(1) : tk_nw(0);
+  const unsigned grid = (unsigned)((n_q + 16 * nw * rg - 1) / (16 * nw * rg));
   const float* scal = reinterpret_cast<const float*>(ws);
   const uint4* vsp4 = reinterpret_cast<const uint4*>(static_cast<char*>(ws) + 256);
   const int32_t* perm =
@@ -31,17 +32,17 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
     if (top <= kTopR) { /* the product picks 8 / 12 / 16 by top: the dev modes use 16 */    \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, kTopR, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, kTopR, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld,  \
+      topk_split_kernel<NK, RG, kTopR, M><<<grid, 64 * nw, lds, st>>>(Q, n_q, vsp4, vsp4 + n_v * (kq / 8), perm, vnorm, n_v, ld,  \
                                                                   k, top, scal, idx, dbg);    \
     } else if (quad) { /* quad lists (rg is 1 here): the dev modes use 100 (configs[4]) */   \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, 1, 100, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, 1, 100, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld,   \
+      topk_split_kernel<NK, 1, 100, M><<<grid, 64 * nw, lds, st>>>(Q, n_q, vsp4, vsp4 + n_v * (kq / 8), perm, vnorm, n_v, ld,   \
                                                                k, top, scal, idx, dbg);       \
     } else {                                                                                  \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, 0, M>), \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-      topk_split_kernel<NK, RG, 0, M><<<grid, 256, lds, st>>>(Q, n_q, vsp4, perm, vnorm, n_v, ld, k, \
+      topk_split_kernel<NK, RG, 0, M><<<grid, 64 * nw, lds, st>>>(Q, n_q, vsp4, vsp4 + n_v * (kq / 8), perm, vnorm, n_v, ld, k, \
                                                               top, scal, idx, dbg);           \
     }                                                                                         \
   } while (0)

@@ -485,7 +485,8 @@ __device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
 // 1 = exact scores only (no filter), 2 = coarse filter against an unbeatable
 // threshold (no refinement, no insertions, no early exit), 3 = as 0 but each wave
 // writes its count of blocks past the coarse filter to score_out[wave] and of
-// tiles swept to score_out[waves + wave] instead of the lists.
+// tiles swept to score_out[waves + wave] instead of the lists; 4 = 2 without the V
+// stream (the first tiles re-staged: compute / LDS only).
 // Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
 // rows), 4 with LDS lists (top > 128: the lists of 64 RG rows fill the LDS).
 __host__ __device__ constexpr int tk_nw(int topr) { return topr > 0 ? 8 : 4; }
@@ -591,34 +592,44 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
 #pragma unroll
   for (int j = 0; j < NR; ++j) kv[j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
 
-  uint4 pre[PER];
-  int pre_p = 0x7fffffff;
+  // Tiles in flight in registers: DEPTH sets; after tile t is scored, tile t + 1 is
+  // staged from set t % DEPTH, which then loads tile t + 1 + DEPTH.  Two sets with
+  // register lists (the sweep is bound by the V bytes in flight), one with LDS lists.
+  constexpr int DEPTH = TOPR > 0 ? 2 : 1;
+  uint4 pre[DEPTH][PER];
+  int pre_p[DEPTH];
   // norm of the first row of the fetched / current tile: V is sorted by decreasing
   // norm, so x 2^(1/128) (one bucket) it bounds every row from that tile on
-  float nv_pre = 0.f, nv_cur = 0.f;
-  auto fetch = [&](int64_t vb) {
+  float nv_pre[DEPTH], nv_cur = 0.f;
+  auto fetch = [&](int64_t vb, auto dc) {
+    constexpr int D = decltype(dc)::value;
+    if (MODE == 4 && vb > 2 * VT) return;  // dev: no V stream (stale tiles re-staged)
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int x = threadIdx.x + NT * e;
       const int64_t vrow = vb + x / RW;
       // rows past n_v: f16 NaNs, so their scores are NaN and never pass a filter
-      pre[e] = vrow < n_v ? Vsp[vrow * RW + x % RW]
-                          : make_uint4(0x7E007E00u, 0x7E007E00u, 0x7E007E00u, 0x7E007E00u);
+      pre[D][e] = vrow < n_v ? Vsp[vrow * RW + x % RW]
+                             : make_uint4(0x7E007E00u, 0x7E007E00u, 0x7E007E00u, 0x7E007E00u);
     }
-    if (threadIdx.x < VT) pre_p = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
-    nv_pre = vnorm[vb];
+    if (threadIdx.x < VT)
+      pre_p[D] = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
+    nv_pre[D] = vnorm[vb];
   };
-  auto stage = [&](int buf) {
+  auto stage = [&](int buf, auto dc) {
+    constexpr int D = decltype(dc)::value;
     uint4* t = tiles + buf * VT * RS;
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int x = threadIdx.x + NT * e;
-      t[(x / RW) * RS + x % RW] = pre[e];
+      t[(x / RW) * RS + x % RW] = pre[D][e];
     }
-    if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p;
-    nv_cur = nv_pre;
+    if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p[D];
+    nv_cur = nv_pre[D];
   };
-  // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m
+  // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m (reading
+  // the B operands one block ahead in registers measured no faster: the sweep is not
+  // bound by LDS latency, and the quad kernel then spills)
   auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {  // hi.hi
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -636,10 +647,12 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   auto refine = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG]) {
     const int64_t vr = ibase + m < n_v ? ibase + m : n_v - 1;  // rows past n_v: NaN anyway
     uint4* scr = loscr + w * NK * 64;
+    if constexpr (MODE != 5) {  // dev MODE 5: stale lo halves, no DMA wait (timing only)
 #pragma unroll
-    for (int s = 0; s < NK; ++s)
-      __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      for (int s = 0; s < NK; ++s)
+        __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
       const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
@@ -688,7 +701,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
 #pragma unroll
         for (int g = 0; g < RG; ++g)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= (MODE == 2 ? 3.0e38f : ts[g][r]);
+          for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= (MODE == 2 || MODE == 4 ? 3.0e38f : ts[g][r]);
         if (__ballot(c) == 0) return;
       }
       refine(tbr, ibase, acc);
@@ -794,63 +807,77 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
     }
   };
 
-  fetch(0);
-  stage(0);
+  using D0 = std::integral_constant<int, 0>;
+  using D1 = std::integral_constant<int, DEPTH - 1>;
+  fetch(0, D0{});
+  stage(0, D0{});
   __syncthreads();
-  if (VT < n_v) fetch(VT);
+  if (VT < n_v) fetch(VT, D0{});
+  if (DEPTH > 1 && 2 * VT < n_v) fetch(2 * VT, D1{});
   int buf = 0;
-  for (int64_t vb = 0; vb < n_v; vb += VT) {
-    const uint4* tb = tiles + buf * VT * RS;
-    nvt = fmaf(nv_cur, 1.01f, 1.f);
-    // early exit: every row of the wave holds a k-th score that no row from this
-    // tile on can reach: k-th > (|q| + 1)(NV + 1)(1 + 2^-7) (dead rows: +inf)
-    bool open = false;
-    if constexpr (TOPR > 0) {
-      if (MODE != 1) refresh();
+  // one tile: score + filter tile vb in buffer buf, stage tile vb + VT from register
+  // set D, barrier, load tile vb + (DEPTH + 1) VT into set D; false: sweep over
+  auto tile_step = [&](int64_t vb, auto dc) -> bool {
+      const uint4* tb = tiles + buf * VT * RS;
+      nvt = fmaf(nv_cur, 1.01f, 1.f);
+      // early exit: every row of the wave holds a k-th score that no row from this
+      // tile on can reach: k-th > (|q| + 1)(NV + 1)(1 + 2^-7) (dead rows: +inf)
+      bool open = false;
+      if constexpr (TOPR > 0) {
+        if (MODE != 1) refresh();
 #pragma unroll
-      for (int g = 0; g < RG; ++g) {
-        const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
-        const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
+        for (int g = 0; g < RG; ++g) {
+          const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
+          const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          open = open || (((live[g] >> (4 * q + r)) & 1u) && !(t4[r] > (0x1p9f + 4.f) * s4[r] * nvt));
-      }
-    } else {
+          for (int r = 0; r < 4; ++r)
+            open = open || (((live[g] >> (4 * q + r)) & 1u) && !(t4[r] > (0x1p9f + 4.f) * s4[r] * nvt));
+        }
+      } else {
 #pragma unroll
-      for (int g = 0; g < RG; ++g) {
-        const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
+        for (int g = 0; g < RG; ++g) {
+          const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) open = open || !(ts[g][r] > (0x1p9f + 4.f) * s4[r] * nvt);
-      }
-    }
-    const bool wdone = (MODE == 0 || MODE == 3) && __ballot(open) == 0;
-    if (!wdone) {
-      if constexpr (MODE == 3) ++n_tiles;
-      floatx4 acc0[RG], acc1[RG];
-      score(tb + m * RS, acc0);
-      // block pairs: issue block c+1's MFMAs, then filter block c
-#pragma unroll 1
-      for (int c = 0; c < NC; c += 2) {
-        const uint4* tbr = tb + (16 * c + m) * RS;
-        const int* bp = tperm + buf * VT + 16 * c;
-        if (NC > 1) score(tbr + 16 * RS, acc1);
-        filter(acc0, vb + 16 * c, bp, tbr);
-        if (NC > 1) {
-          if (c + 2 < NC) score(tbr + 32 * RS, acc0);
-          filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
+          for (int r = 0; r < 4; ++r) open = open || !(ts[g][r] > (0x1p9f + 4.f) * s4[r] * nvt);
         }
       }
-    }
-    if (vb + VT < n_v) stage(buf ^ 1);
-    if (lane == 0) sdone[buf * NW + w] = wdone ? 1 : 0;
-    __syncthreads();
-    // (flags of this buffer are rewritten only after the next barrier)
-    int alldone = 1;
+      const bool wdone = (MODE == 0 || MODE == 3) && __ballot(open) == 0;
+      if (!wdone) {
+        if constexpr (MODE == 3) ++n_tiles;
+        floatx4 acc0[RG], acc1[RG];
+        score(tb + m * RS, acc0);
+        // block pairs: issue block c+1's MFMAs, then filter block c
+#pragma unroll 1
+        for (int c = 0; c < NC; c += 2) {
+          const uint4* tbr = tb + (16 * c + m) * RS;
+          const int* bp = tperm + buf * VT + 16 * c;
+          if (NC > 1) score(tbr + 16 * RS, acc1);
+          filter(acc0, vb + 16 * c, bp, tbr);
+          if (NC > 1) {
+            if (c + 2 < NC) score(tbr + 32 * RS, acc0);
+            filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
+          }
+        }
+      }
+      if (vb + VT < n_v) stage(buf ^ 1, dc);
+      if (lane == 0) sdone[buf * NW + w] = wdone ? 1 : 0;
+      __syncthreads();
+      // (flags of this buffer are rewritten only after the next barrier)
+      int alldone = 1;
 #pragma unroll
-    for (int i = 0; i < NW; ++i) alldone &= sdone[buf * NW + i];
-    if (alldone) break;
-    if (vb + 2 * VT < n_v) fetch(vb + 2 * VT);
-    buf ^= 1;
+      for (int i = 0; i < NW; ++i) alldone &= sdone[buf * NW + i];
+      if (alldone) return false;
+      if (vb + (DEPTH + 1) * VT < n_v) fetch(vb + (DEPTH + 1) * VT, dc);
+      buf ^= 1;
+      return vb + VT < n_v;
+  };
+  for (int64_t vb = 0;;) {
+    if (!tile_step(vb, D0{})) break;
+    vb += VT;
+    if constexpr (DEPTH > 1) {
+      if (!tile_step(vb, D1{})) break;
+      vb += VT;
+    }
   }
   if constexpr (MODE != 0) {
     if (lane == 0) score_out[blockIdx.x * NW + w] = MODE == 1 ? sink : (float)n_offer;

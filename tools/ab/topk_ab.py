@@ -18,7 +18,7 @@ from als_mi355x import datasets as D, engine as E  # noqa: E402
 
 def main():
     s = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
-    variants = sys.argv[2:] or ["base", "new"]
+    variants = sys.argv[2:] or open(os.path.join(ROOT, "tools", "ab", "variants.txt")).read().split()
     dev = torch.device("cuda", 0)
     u, i, r = D.big_config("big1b", device=dev)
     core = E.ALSCore(u, i, r, device=dev)

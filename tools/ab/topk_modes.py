@@ -40,7 +40,7 @@ def main():
         sc = torch.empty((s, top), dtype=torch.float32, device=dev)
         dbg = torch.zeros(s * 8 + 64, dtype=torch.float32, device=dev)
         st = torch.cuda.current_stream().cuda_stream
-        for mode in (0, 1, 2, 3, 0):
+        for mode in (0, 1, 2, 4, 5, 3, 0):
             args = (mode, Q.data_ptr(), s, core.V.data_ptr(), n_v, Q.shape[1], 128, top,
                     idx.data_ptr(), sc.data_ptr(), ws.data_ptr(), ws.numel(), dbg.data_ptr(), st)
             assert L.dev_topk(*args) == 0

@@ -52,6 +52,10 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
       L(NK, RG, 1); \
     else if (mode == 2) \
       L(NK, RG, 2); \
+    else if (mode == 4) \
+      L(NK, RG, 4); \
+    else if (mode == 5) \
+      L(NK, RG, 5); \
     else           \
       L(NK, RG, 3); \
   } while (0)

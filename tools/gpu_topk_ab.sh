@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --time
 rc=$?
 grep -E "PASSED|FAILED|ERROR|passed|failed" $OUT/tests.log | tail -60
 [ $rc -ne 0 ] && { grep -E "^E |Error" $OUT/tests.log | head -40; exit $rc; }
-timeout -k 10 400 python -u tools/ab/topk_ab.py $S base new > $OUT/ab.log 2>&1
+timeout -k 10 400 python -u tools/ab/topk_ab.py $S > $OUT/ab.log 2>&1
 rc=$?
 cat $OUT/ab.log | grep -v Warning | tail -20
 exit $rc

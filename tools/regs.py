@@ -1,6 +1,7 @@
 """Dev: per-kernel register / occupancy / spill table of one HIP source (gfx950),
 from clang's kernel-resource-usage remarks.
     python tools/regs.py path/to/file.hip [name-filter]"""
+import os
 import re
 import subprocess
 import sys
@@ -9,7 +10,7 @@ import sys
 def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
-    inc = "-I" + src.rsplit("/", 1)[0] if "/" in src else "-I."
+    inc = "-I" + os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "recommender-system-using-apache-spark-mllib-_amd", "csrc")
     p = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", inc,
                         "-c", src, "-o", "/tmp/_regs.o", "-Rpass-analysis=kernel-resource-usage"],
                        capture_output=True, text=True)

@@ -120,7 +120,7 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * the largest n_chunks).
  * n_light_primal (0 <= n_light_primal <= n_light): the first n_light_primal light
  * rows are solved on the k x k normal equations above; the remaining light rows
- * (the tail of the longest-first light list) must have <= 64 ratings and are
+ * (the tail of the longest-first light list) must have <= 96 ratings and are
  * solved through the equivalent n x n dual system (push-through identity
  * (Y^T Y + lambda n I)^-1 Y^T r = Y^T (Y Y^T + lambda n I)^-1 r), allowed for
  * explicit feedback, 64 < k <= 128, reg > 0 only.  n_light_primal = n_light
@@ -172,10 +172,14 @@ int als_rmse_partial(const int32_t* u, const int32_t* i, const float* r, int64_t
  * idx_out[n_q*top] (dense row index of V, -1 when n_v < top), score_out[n_q*top].
  * Scores: fp32-grade products on the f16 matrix cores (q and v split into f16
  * hi + lo after power-of-two scaling, ~2^-21 relative to |q||v|) for every k and
- * top.  Lists: registers of one owner lane for top <= 16, four-lane ("quad")
- * register lists for top <= 128, sorted LDS lists above.  k <= 128, top <= 256.
- * The n_q x n_v score matrix is never materialised.
- * Workspace (16-byte aligned): scale words + the split copy of V. */
+ * top: V is swept with hi.hi alone against the row's k-th score minus a proven
+ * bound on the dropped terms, and blocks past it get the full hi.hi + hi.lo + lo.hi
+ * score, so every listed pair carries its exact split score.  Lists: registers of
+ * one owner lane for top <= 16, four-lane ("quad") register lists for top <= 128,
+ * sorted LDS lists above.  Rows of V holding NaN score NaN and are never listed.
+ * k <= 128, top <= 256.  The n_q x n_v score matrix is never materialised.
+ * Workspace (16-byte aligned): scale words, the hi and lo f16 planes of V in sweep
+ * (decreasing norm) order, the order, bucket counts and the scaled row norms. */
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top);
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v,
              int32_t ld, int32_t k, int32_t top,

@@ -1004,9 +1004,15 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 // two groups must still leave room for two workgroups per CU: the list inserts
 // are latency-bound and need the second workgroup (measured, configs[4] top-100
 // at rank 128: one 120 KB workgroup per CU 602 ms, two 68 KB ones 480 ms).
-static int topk_split_rg(int k, int top, bool quad) {
+// Register lists take two groups (256 query rows per 8-wave workgroup) only when
+// that still gives >= 4 workgroups per CU: measured top-10, ML-25M shape (162,541
+// users, rank 64) 4.7 ms with two groups, 3.6 ms with one (the tail of 2.5 rounds);
+// configs[4] (262,144-user sample, rank 128) 97 ms with two, 151 ms with one.
+constexpr int64_t kTkRg2MinRows = 4 * 256 * 256;
+static int topk_split_rg(int k, int top, bool quad, int64_t n_q) {
   const int kq = topk_kq(k);
   if (quad) return 1;  // quad lists: one row group
+  if (top <= kTopR && n_q < kTkRg2MinRows) return 1;
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
   if (topk_split_lds_bytes(kq, 1, top, false) <= (size_t)kLdsBytes) return 1;
@@ -1046,7 +1052,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   ALS_REQUIRE(Q && V && idx_out && score_out, ALS_EINVAL, "als_topk: null pointer");
   hipStream_t st = as_stream(stream);
   const bool quad = topk_quad(top, n_v);
-  const int rg = topk_split_rg(k, top, quad);
+  const int rg = topk_split_rg(k, top, quad, n_q);
   ALS_REQUIRE(rg > 0, ALS_EUNSUPPORTED, "als_topk: top %d at rank %d does not fit the LDS", top,
               k);
   ALS_REQUIRE(ws != nullptr && ws_bytes >= als_topk_workspace_bytes(n_q, n_v, k, top),

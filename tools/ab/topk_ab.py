@@ -17,17 +17,20 @@ from als_mi355x import datasets as D, engine as E  # noqa: E402
 
 
 def main():
-    s = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
+    ml = len(sys.argv) > 1 and sys.argv[1] == "ml25m"  # configs[1] shape, rank 64, all users
+    s = 0 if ml else (int(sys.argv[1]) if len(sys.argv) > 1 else 262144)
     variants = sys.argv[2:] or open(os.path.join(ROOT, "tools", "ab", "variants.txt")).read().split()
     dev = torch.device("cuda", 0)
-    u, i, r = D.big_config("big1b", device=dev)
+    k = 64 if ml else 128
+    u, i, r = D.synthetic_config("ml25m", device=dev) if ml else D.big_config("big1b", device=dev)
     core = E.ALSCore(u, i, r, device=dev)
     del u, i, r
     torch.cuda.empty_cache()
-    core.init_factors(128, seed=5)
+    core.init_factors(k, seed=5)
     for _ in range(2):
         core.iterate(0.1)
     torch.cuda.synchronize()
+    s = s or core.n_users
     Q = core.U[:s].contiguous()
     V = core.V
     n_v = core.n_items
@@ -40,11 +43,11 @@ def main():
         L.ab_ws.argtypes = [I64, I64, ctypes.c_int, ctypes.c_int]
         L.ab_ws.restype = ctypes.c_size_t
         for top in (10, 100):
-            ws = torch.empty(int(L.ab_ws(s, n_v, 128, top)) + 4096, dtype=torch.uint8, device=dev)
+            ws = torch.empty(int(L.ab_ws(s, n_v, k, top)) + 4096, dtype=torch.uint8, device=dev)
             idx = torch.empty((s, top), dtype=torch.int32, device=dev)
             sc = torch.empty((s, top), dtype=torch.float32, device=dev)
             st = torch.cuda.current_stream().cuda_stream
-            args = (Q.data_ptr(), s, V.data_ptr(), n_v, 128, 128, top, idx.data_ptr(),
+            args = (Q.data_ptr(), s, V.data_ptr(), n_v, Q.shape[1], k, top, idx.data_ptr(),
                     sc.data_ptr(), ws.data_ptr(), ws.numel(), st)
             assert L.ab_topk(*args) == 0
             torch.cuda.synchronize()

@@ -16,7 +16,7 @@ extern "C" int dev_topk(int mode, const float* Q, int64_t n_q, const float* V, i
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int kq = topk_kq(k);
   const bool quad = topk_quad(top, n_v);
-  const int rg = topk_split_rg(k, top, quad);
+  const int rg = topk_split_rg(k, top, quad, n_q);
   if (rg == 0) return -1;
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
   const int nw = (top <= kTopR || quad) ? tk_nw(1) : tk_nw(0);

@@ -147,13 +147,35 @@ def _pmc_view(pmc, t_s):
     return v
 
 
+def _combine_pmc(workload: str, parts):
+    """Counter view of one launch-1 phase made of several kernels [(kernel, grid)]:
+    summed traffic and durations, busy fractions weighted by each kernel's time."""
+    ents = [load_pmc(workload, kern, grid) for kern, grid in parts]
+    ents = [e for e in ents if e]
+    if not ents or len(ents) < len(parts):
+        return None
+    if len(ents) == 1:
+        return ents[0]
+    out = {}
+    for key in ("fetch_bytes_x2", "write_bytes", "pmc_run_avg_ns", "trace_avg_ns", "mfma_flop_f16"):
+        if all(key in e for e in ents):
+            out[key] = sum(e[key] for e in ents)
+    tw = [e.get("pmc_run_avg_ns", 0.0) for e in ents]
+    for key in ("mfma_busy_frac", "valu_busy_frac"):
+        if all(key in e for e in ents) and sum(tw) > 0:
+            out[key] = sum(e[key] * t for e, t in zip(ents, tw)) / sum(tw)
+    return out
+
+
 def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool):
-    """Roofline of launch 1 of each half-sweep (the fused Gram + solve kernel).
-    launches: {"item"|"user": {"ms": HIP-event average on the launching stream,
-    "nnz": ratings, "rows": rows solved in the launch, "grid": grid threads}}.
-    achieved = algorithmic bytes (or issued flops) / event time; frac_rocprof uses the
-    rocprofv3 kernel-trace average of the same launch instead; traffic / busy
-    fractions / limiter come from that workload's PMC passes."""
+    """Roofline of launch 1 of each half-sweep (the fused Gram + solve kernel; at
+    64 < k <= 128 explicit, the n x n dual kernel of the short rows runs in the same
+    phase).  launches: {"item"|"user": {"ms": HIP-event average of the phase on the
+    launching stream, "nnz": ratings, "rows": rows solved in the phase, "parts":
+    [(kernel, grid threads)]}}.  achieved = algorithmic bytes (or modelled issued flops:
+    the primal k x k Gram + solve for every row) / event time; frac_rocprof uses the
+    rocprofv3 kernel-trace durations of the same kernels instead; traffic / busy
+    fractions / limiter / counted MFMA flops come from that workload's PMC passes."""
     out = {"kernel": kernel, "launches": {}}
     tb = tf = tfa = te = tr = 0.0
     traffic = 0.0
@@ -167,10 +189,13 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
         ent = {"event_ms": L["ms"], "algorithmic_bytes": b, "hbm_gbs": b / t / 1e9,
                "hbm_frac": b / t / 1e9 / PEAK_HBM_GBS, "mfma_issued_flops": fm,
                "mfma_frac": fm / t / 1e12 / PEAK_F16_MFMA_TFLOPS,
-               "fp32_grade_tflops": fa / t / 1e12, "grid_threads": L["grid"]}
-        pv = _pmc_view(load_pmc(workload, kernel, L["grid"]), t)
+               "fp32_grade_tflops": fa / t / 1e12, "kernels": [list(x) for x in L["parts"]]}
+        pv = _pmc_view(_combine_pmc(workload, L["parts"]), t)
         if pv:
             ent["pmc"] = pv
+            if pv.get("mfma_flop_f16"):  # counted f16 MFMA flops of the phase's kernels
+                ent["mfma_issued_flops_pmc"] = pv["mfma_flop_f16"]
+                ent["mfma_frac_pmc"] = pv["mfma_flop_f16"] / t / 1e12 / PEAK_F16_MFMA_TFLOPS
             if pv.get("trace_avg_ns"):
                 ent["rocprof_ms"] = pv["trace_avg_ns"] * 1e-6
                 ent["hbm_frac_rocprof"] = b / (pv["trace_avg_ns"] * 1e-9) / 1e9 / PEAK_HBM_GBS
@@ -370,8 +395,17 @@ def _iteration(core, k, reg, imp, alpha, evs=None):
                       evs[2:4] if evs else None)
 
 
-def _launch1_grid(block) -> int:
-    return 64 * (block.n_chunks + block.n_light)
+def _launch1_parts(block, k: int, imp: bool):
+    """Kernels of launch-1 phase of a half-sweep, as als_solve_half launches them:
+    [(kernel, grid threads)] (engine.solve_half: the dual kernel for the short explicit
+    rows at 64 < k <= 128)."""
+    kern = dominant_kernel(k, imp)
+    dual = (not imp) and k > 64 and block.n_short > 0
+    n_primal = block.n_light - block.n_short if dual else block.n_light
+    parts = [(kern, 64 * (block.n_chunks + n_primal))]
+    if dual:
+        parts.append(("gram_solve_dual_kernel", 64 * block.n_short))
+    return parts
 
 
 def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
@@ -392,10 +426,13 @@ def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
     ib, ub = core.item_block, core.user_block
     launches = {
         "item": {"ms": sum(e[0].elapsed_time(e[1]) for e in evs) / steps, "nnz": ib.nnz,
-                 "rows": ib.n_light, "grid": _launch1_grid(ib)},
+                 "rows": ib.n_light, "parts": _launch1_parts(ib, k, imp)},
         "user": {"ms": sum(e[2].elapsed_time(e[3]) for e in evs) / steps, "nnz": ub.nnz,
-                 "rows": ub.n_light, "grid": _launch1_grid(ub)}}
-    return 1e3 * dt, roofline(workload, dominant_kernel(k, imp), launches, k, imp)
+                 "rows": ub.n_light, "parts": _launch1_parts(ub, k, imp)}}
+    kern = dominant_kernel(k, imp)
+    if any(len(L["parts"]) > 1 for L in launches.values()):
+        kern += " + gram_solve_dual_kernel"
+    return 1e3 * dt, roofline(workload, kern, launches, k, imp)
 
 
 def configs2(core, args):
@@ -447,8 +484,8 @@ def big_single(args, dev, want_c3=True, want_c4=True):
             ms = _timed_topk(core.U, core.n_users, core.V, core.n_items, k, top)
             c4[f"top{top}_recs_per_s"] = core.n_users / (ms * 1e-3)
             c4[f"top{top}_ms"] = ms
-            c4[f"top{top}_roofline"] = topk_roofline(f"configs4_top{top}", core.n_users,
-                                                     core.n_items, k, ms, top)
+            c4[f"top{top}_roofline"] = topk_roofline("configs4", core.n_users, core.n_items, k,
+                                                     ms, top)
     del core
     torch.cuda.empty_cache()
     return c3, c4
@@ -506,8 +543,7 @@ def run_single(args):
         "roofline": roof,
         "topk10_recs_per_s": core.n_users / (topk_ms * 1e-3),
         "topk10_ms": topk_ms,
-        "topk_roofline": topk_roofline("configs1_top10", core.n_users, core.n_items, k, topk_ms,
-                                       10),
+        "topk_roofline": topk_roofline("configs1", core.n_users, core.n_items, k, topk_ms, 10),
         "csr_build_ms": build_ms,
         "datagen_s": t_gen,
         "schedule": {"item": [ib.n_light, ib.n_heavy, ib.n_chunks],

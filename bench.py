@@ -253,16 +253,19 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
     return out
 
 
-def topk_variant(k: int, top: int, n_q: int) -> str:
-    """The kernel als_topk launches (csrc/topk.hip): <NK, row groups, list kind, 0>."""
+def topk_variant(k: int, top: int, n_q: int):
+    """The kernel als_topk launches (csrc/topk.hip) and its grid in threads:
+    (<NK, row groups, list kind, 0>, grid)."""
     nk = max(32, kp_of(k)) // 32
     if top <= 16:  # two row groups from 4 x 256 x 256 query rows (topk_split_rg)
         rg, tr = (2 if n_q >= 4 * 256 * 256 else 1), (8 if top <= 8 else (12 if top <= 12 else 16))
     elif top <= 128:  # quad register lists, one row group
         rg, tr = 1, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
     else:
-        return f"topk_split_kernel<{nk},?,0,0>"
-    return f"topk_split_kernel<{nk},{rg},{tr},0>"
+        return f"topk_split_kernel<{nk},?,0,0>", None
+    nw = 8  # wavefronts per workgroup with register lists (tk_nw)
+    grid = (n_q + 16 * nw * rg - 1) // (16 * nw * rg) * 64 * nw
+    return f"topk_split_kernel<{nk},{rg},{tr},0>", grid
 
 
 def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int):
@@ -275,7 +278,7 @@ def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int
     kq = max(32, kp_of(k))  # topk_kq (csrc/topk.hip): dims padded to 32/64/128
     coarse = 2.0 * n_q * n_v * kq
     s = ms * 1e-3
-    kern = topk_variant(k, top, n_q)
+    kern, grid = topk_variant(k, top, n_q)
     out = {"kernel": kern, "top": top, "n_q": n_q, "n_v": n_v, "rank": k,
            "ms": ms, "recs_per_s": n_q / s,
            "useful_fp32_grade_tflops": useful / s / 1e12,
@@ -283,7 +286,7 @@ def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int
            "bound": "mfma", "achieved": coarse / s / 1e12, "peak": PEAK_F16_MFMA_TFLOPS,
            "unit": "TFLOP/s", "frac": coarse / s / 1e12 / PEAK_F16_MFMA_TFLOPS,
            "algorithmic_bytes": 4.0 * (n_q + n_v) * k + 8.0 * n_q * top}
-    pv = _pmc_view(load_pmc(workload, kern), s)
+    pv = _pmc_view(load_pmc(workload, kern, grid), s)
     if pv:
         out["pmc"] = pv
         out["traffic"] = pv.get("traffic_bytes")
@@ -471,9 +474,9 @@ def big_single(args, dev, want_c3=True, want_c4=True):
                                     core.item_block.n_chunks],
                            "user": [core.user_block.n_light, core.user_block.n_heavy,
                                     core.user_block.n_chunks]}}
-    else:
+    else:  # the factor state the full run reaches: seed + 1 warmup + `steps` iterations
         core.init_factors(k, seed=5)
-        for _ in range(2):
+        for _ in range(1 + steps):
             core.iterate(args.reg)
         torch.cuda.synchronize()
     if want_c4:

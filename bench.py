@@ -401,13 +401,12 @@ def _iteration(core, k, reg, imp, alpha, evs=None):
 def _launch1_parts(block, k: int, imp: bool):
     """Kernels of launch-1 phase of a half-sweep, as als_solve_half launches them:
     [(kernel, grid threads)] (engine.solve_half: the dual kernel for the short explicit
-    rows at 64 < k <= 128)."""
+    rows at 32 < k <= 128)."""
     kern = dominant_kernel(k, imp)
-    dual = (not imp) and k > 64 and block.n_short > 0
-    n_primal = block.n_light - block.n_short if dual else block.n_light
-    parts = [(kern, 64 * (block.n_chunks + n_primal))]
-    if dual:
-        parts.append(("gram_solve_dual_kernel", 64 * block.n_short))
+    n_dual = 0 if imp else block.n_dual(k)
+    parts = [(kern, 64 * (block.n_chunks + block.n_light - n_dual))]
+    if n_dual > 0:
+        parts.append((f"gram_solve_dual_kernel<{128 if k > 64 else 64}>", 64 * n_dual))
     return parts
 
 
@@ -434,7 +433,7 @@ def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
                  "rows": ub.n_light, "parts": _launch1_parts(ub, k, imp)}}
     kern = dominant_kernel(k, imp)
     if any(len(L["parts"]) > 1 for L in launches.values()):
-        kern += " + gram_solve_dual_kernel"
+        kern += " + " + next(p[0] for L in launches.values() for p in L["parts"][1:])
     return 1e3 * dt, roofline(workload, kern, launches, k, imp)
 
 

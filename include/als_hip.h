@@ -120,11 +120,12 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * the largest n_chunks).
  * n_light_primal (0 <= n_light_primal <= n_light): the first n_light_primal light
  * rows are solved on the k x k normal equations above; the remaining light rows
- * (the tail of the longest-first light list) must have <= 96 ratings and are
- * solved through the equivalent n x n dual system (push-through identity
- * (Y^T Y + lambda n I)^-1 Y^T r = Y^T (Y Y^T + lambda n I)^-1 r), allowed for
- * explicit feedback, 64 < k <= 128, reg > 0 only.  n_light_primal = n_light
- * keeps every row on the primal path. */
+ * (the tail of the longest-first light list) must have <= 96 ratings (64 < k <= 128)
+ * or <= 32 ratings (32 < k <= 64) and are solved through the equivalent n x n dual
+ * system (push-through identity (Y^T Y + lambda n I)^-1 Y^T r =
+ * Y^T (Y Y^T + lambda n I)^-1 r), allowed for explicit feedback, 32 < k <= 128,
+ * reg > 0 only (a longer row there is reported through status_dev).
+ * n_light_primal = n_light keeps every row on the primal path. */
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src);
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light, int32_t n_light_primal,

@@ -1931,16 +1931,20 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
 //    (z_lo, z_lo) (z split after a power-of-two scale) accumulates (hi + lo) z in
 //    fp32; summed over the 16 lanes of a row group.
 // NB = 2 (n <= 32), 4 (n <= 64), 6 (n <= 96): a wave-uniform branch of one kernel.
+// 32 < k <= 64 (KP = 64 split words per row): n <= 32 only (NB = 2 against the primal
+// NB = 4: a quarter of the k x k Gram tiles, half the block sweeps; for 32 < n <= 64
+// the dual system is as large as the primal one).
 constexpr int kDualMaxRatings = 96;
+constexpr int kDualMaxRatings64 = 32;
 
 // The 8 split words of dims 32s + 8q .. +7 of each operand block's rating.
-template <int NB>
+template <int NB, int KP>
 __device__ __forceinline__ void dual_gather_step(uint32_t (&w)[NB][8], const int (&cc)[NB], int s,
                                                  const uint32_t* __restrict__ Ysp) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int c = 0; c < NB; ++c) {
-    const uint32_t* p = Ysp + (uint64_t)(uint32_t)cc[c] * 128u + 32 * s + 8 * q;
+    const uint32_t* p = Ysp + (uint64_t)(uint32_t)cc[c] * (uint32_t)KP + 32 * s + 8 * q;
     const uint4 a = *reinterpret_cast<const uint4*>(p);
     const uint4 b = *reinterpret_cast<const uint4*>(p + 4);
     w[c][0] = a.x; w[c][1] = a.y; w[c][2] = a.z; w[c][3] = a.w;
@@ -1948,12 +1952,13 @@ __device__ __forceinline__ void dual_gather_step(uint32_t (&w)[NB][8], const int
   }
 }
 
-template <int NB>
+template <int NB, int KP>
 __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
                                          const float (&rj)[2], const uint32_t* __restrict__ Ysp,
                                          int ey, float reg, float* __restrict__ xrow, int ld,
                                          float* __restrict__ lds, int32_t* __restrict__ status) {
   constexpr int NT = NB * (NB + 1) / 2;
+  constexpr int NS = KP / 32;  // k-steps of 32 dims
   typedef FullTiles<NB> TS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   // operand block c of lane (q, m) is rating j = m * NB + c (held by lane j % 64 in
@@ -1982,12 +1987,13 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   // registers (the two waves per SIMD overlap each other's gathers instead)
   constexpr int NBUF = NB <= 4 ? 2 : 1;
   uint32_t w[NBUF][NB][8];
-  dual_gather_step<NB>(w[0], cc, 0, Ysp);
-  static_for<4>([&](auto sc) {
+  dual_gather_step<NB, KP>(w[0], cc, 0, Ysp);
+  static_for<NS>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     constexpr int cur = s % NBUF;
-    if constexpr (NBUF == 2 && s + 1 < 4) dual_gather_step<NB>(w[(s + 1) % NBUF], cc, s + 1, Ysp);
-    if constexpr (NBUF == 1 && s > 0) dual_gather_step<NB>(w[0], cc, s, Ysp);
+    if constexpr (NBUF == 2 && s + 1 < NS)
+      dual_gather_step<NB, KP>(w[(s + 1) % NBUF], cc, s + 1, Ysp);
+    if constexpr (NBUF == 1 && s > 0) dual_gather_step<NB, KP>(w[0], cc, s, Ysp);
     uint32_t hi[NB][4], lo[NB][4];
 #pragma unroll
     for (int c = 0; c < NB; ++c)
@@ -2041,13 +2047,14 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
     zh2[c] = half2v{h, h};
     zl2[c] = half2v{l, l};
   }
-  float px[4][8];
-  dual_gather_step<NB>(w[0], cc, 0, Ysp);
-  static_for<4>([&](auto sc) {
+  float px[NS][8];
+  dual_gather_step<NB, KP>(w[0], cc, 0, Ysp);
+  static_for<NS>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     constexpr int cur = s % NBUF;
-    if constexpr (NBUF == 2 && s + 1 < 4) dual_gather_step<NB>(w[(s + 1) % NBUF], cc, s + 1, Ysp);
-    if constexpr (NBUF == 1 && s > 0) dual_gather_step<NB>(w[0], cc, s, Ysp);
+    if constexpr (NBUF == 2 && s + 1 < NS)
+      dual_gather_step<NB, KP>(w[(s + 1) % NBUF], cc, s + 1, Ysp);
+    if constexpr (NBUF == 1 && s > 0) dual_gather_step<NB, KP>(w[0], cc, s, Ysp);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       float a = 0.f;
@@ -2064,7 +2071,7 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   const float un = ldexpf(1.f, -ey - ez);
   if (m == 0) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+    for (int s = 0; s < NS; ++s)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int d = 32 * s + 8 * q + 4 * h;
@@ -2077,20 +2084,24 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
 }
 
 // One wavefront per short light row (the tail of the longest-first light list: every
-// row with <= kDualMaxRatings ratings), explicit, k in (64, 128], regParam > 0.
+// row with <= kDualMaxRatings ratings at k in (64, 128], KP = 128; <= kDualMaxRatings64
+// at k in (32, 64], KP = 64), explicit, regParam > 0.
+template <int KP>
 __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
     float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
     const uint32_t* __restrict__ Ysp, int32_t zero_row) {
-  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<6>::SIZE];
+  static_assert(KP == 64 || KP == 128, "dual: k_pad 64 or 128");
+  constexpr int NMAX = KP == 128 ? kDualMaxRatings : kDualMaxRatings64;
+  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<KP == 128 ? 6 : 2>::SIZE];
   const int lane = threadIdx.x & 63;
   const int row = rows[blockIdx.x];
   const int64_t pb = row_ptr[row];
   const int n = (int)(row_ptr[row + 1] - pb);
   const int ey = split_exponent(scal[0]);
   float* xrow = X + (int64_t)row * ld;
-  if (n > kDualMaxRatings) {  // schedule contract broken: report the row, leave it zero
+  if (n > NMAX) {  // schedule contract broken: report the row, leave it zero
     if (lane == 0) atomicCAS(status, 0, row + 1);
     return;
   }
@@ -2103,12 +2114,16 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     cj[h] = j < n ? col[pb + j] : zero_row;
     rj[h] = j < n ? val[pb + j] : 0.f;
   }
-  if (n <= 32)
-    dual_row<2>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
-  else if (n <= 64)
-    dual_row<4>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
-  else
-    dual_row<6>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+  if constexpr (KP == 64) {
+    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+  } else {
+    if (n <= 32)
+      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+    else if (n <= 64)
+      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+    else
+      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+  }
 }
 
 // Launch 2 (W1): heavy rows — fp64 sums of the fp32 chunk partials in a fixed
@@ -2353,9 +2368,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
               "als_solve_half: negative counts");
   ALS_REQUIRE(n_light_primal >= 0 && n_light_primal <= n_light, ALS_EINVAL,
               "als_solve_half: n_light_primal %d not in [0, n_light=%d]", n_light_primal, n_light);
-  ALS_REQUIRE(n_light_primal == n_light || (!implicit && k > 64 && reg > 0.f), ALS_EINVAL,
+  ALS_REQUIRE(n_light_primal == n_light || (!implicit && k > 32 && reg > 0.f), ALS_EINVAL,
               "als_solve_half: the dual path (light rows past n_light_primal) is for explicit "
-              "feedback at rank 65-128 with regParam > 0 only");
+              "feedback at rank 33-128 with regParam > 0 only");
   ALS_REQUIRE(Y_src && X_dst && row_ptr && status_dev, ALS_EINVAL, "als_solve_half: null pointer");
   ALS_REQUIRE(!implicit || yty_packed, ALS_EINVAL, "als_solve_half: implicit needs yty_packed");
   ALS_REQUIRE(reg >= 0.f && alpha >= 0.f, ALS_EINVAL, "als_solve_half: reg/alpha must be >= 0");
@@ -2420,10 +2435,17 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   do {                                                                                            \
     if (g1)                                                                                       \
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
-                                                    chunk_begin, chunk_end, n_chunks, n_light,    \
-                                                    Y_src, X_dst, ld, k, reg, alpha, yty_packed,  \
-                                                    slots, status_dev, scal, Ysp, kp, zero_row);  \
+                                                    chunk_begin, chunk_end, n_chunks,             \
+                                                    n_light_primal, Y_src, X_dst, ld, k, reg,     \
+                                                    alpha, yty_packed, slots, status_dev, scal,   \
+                                                    Ysp, kp, zero_row);                           \
     ALS_LAUNCH_CHECK();                                                                           \
+    if (gd && CN == 4 && !IMP) {                                                                  \
+      gram_solve_dual_kernel<64><<<gd, 64, 0, st>>>(row_ptr, col, val,                            \
+                                                    light_rows + n_light_primal, X_dst, ld, reg,  \
+                                                    status_dev, scal, Ysp, zero_row);             \
+      ALS_LAUNCH_CHECK();                                                                         \
+    }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_f64_kernel<Cfg<CN>::SLOT>                                                         \
           <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots);       \
@@ -2444,8 +2466,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                    status_dev, scal, Ysp, kp, zero_row);          \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd) {                                                                                     \
-      gram_solve_dual_kernel<<<gd, 64, 0, st>>>(row_ptr, col, val, light_rows + n_light_primal,   \
-                                                X_dst, ld, reg, status_dev, scal, Ysp, zero_row); \
+      gram_solve_dual_kernel<128><<<gd, 64, 0, st>>>(row_ptr, col, val,                           \
+                                                     light_rows + n_light_primal, X_dst, ld, reg, \
+                                                     status_dev, scal, Ysp, zero_row);            \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
     if (g2) {                                                                                     \

@@ -29,6 +29,7 @@ from ._lib import check, ptr, stream_ptr
 DEFAULT_CHUNK = 2048  # ratings per heavy-row task
 MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
 DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
+DUAL_MAX_RATINGS_64 = 32  # explicit, 32 < k <= 64: the same for rows this short
 
 
 def ld_for(rank: int) -> int:
@@ -149,6 +150,11 @@ class RatingBlock:
     chunk_begin: torch.Tensor
     chunk_end: torch.Tensor
     n_short: int = 0  # light rows with <= DUAL_MAX_RATINGS ratings (the light list's tail)
+    n_short64: int = 0  # light rows with <= DUAL_MAX_RATINGS_64 ratings
+
+    def n_dual(self, rank: int) -> int:
+        """Light rows solved through the n x n dual system at this rank (explicit, reg > 0)."""
+        return self.n_short if rank > 64 else (self.n_short64 if rank > 32 else 0)
 
 
 def build_block(row_ids: torch.Tensor, row_index: IdIndex, col_ids: torch.Tensor,
@@ -188,12 +194,14 @@ def schedule_block(n_rows, nnz, row_ptr, col, val, ws: Workspace, chunk: int = D
                                ptr(light), ptr(heavy), ptr(slot_begin), ptr(crow), ptr(cbeg),
                                ptr(cend), ptr(w), w.numel(), stream_ptr(dev)),
           "als_schedule_build")
-    n_short = 0
+    n_short = n_short64 = 0
     if n_light > 0:  # light rows are ordered by decreasing degree: the short ones are last
         lr = light[:n_light].long()
-        n_short = int(((row_ptr[lr + 1] - row_ptr[lr]) <= DUAL_MAX_RATINGS).sum())
+        deg = row_ptr[lr + 1] - row_ptr[lr]
+        n_short = int((deg <= DUAL_MAX_RATINGS).sum())
+        n_short64 = int((deg <= DUAL_MAX_RATINGS_64).sum())
     return RatingBlock(n_rows, nnz, row_ptr, col, val, chunk, n_light, n_heavy, n_chunks, light,
-                       heavy, slot_begin, crow, cbeg, cend, n_short)
+                       heavy, slot_begin, crow, cbeg, cend, n_short, n_short64)
 
 
 # ---------------------------------------------------------------------------
@@ -222,12 +230,13 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
     phases (bits, see als_hip.h): 4 = Y prep (max |Y|, split table), 8 = rating scale,
     1 = launch 1, 2 = launch 2; 15 = all in order.  ws_chunks: size the workspace for
     this many heavy-row chunks (>= block.n_chunks; blocks sharing one Y prep).
-    dual: explicit, 64 < rank <= 128, reg > 0 — rows with <= DUAL_MAX_RATINGS ratings
-    are solved through the equivalent n x n dual system (als_hip.h n_light_primal);
-    False keeps every row on the k x k normal equations."""
+    dual: explicit, reg > 0 — rows with <= DUAL_MAX_RATINGS ratings (64 < rank <= 128)
+    or <= DUAL_MAX_RATINGS_64 (32 < rank <= 64) are solved through the equivalent
+    n x n dual system (als_hip.h n_light_primal); False keeps every row on the k x k
+    normal equations."""
     L = _lib.lib()
-    use_dual = dual and not implicit and rank > 64 and reg > 0
-    n_primal = block.n_light - block.n_short if use_dual else block.n_light
+    use_dual = dual and not implicit and reg > 0
+    n_primal = block.n_light - block.n_dual(rank) if use_dual else block.n_light
     w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0]),
                keep_scale=True)
     key = (w.data_ptr(), w.numel())

@@ -79,7 +79,7 @@ def _solve_args(**over):
     (dict(n_light=-1), -1), (dict(Y=0), -1), (dict(implicit=1), -1), (dict(reg=-1.0), -1),
     (dict(Y=18), -1), (dict(phases=0), -1), (dict(phases=16), -1), (dict(n_src=-1), -1), (dict(ws=8), -1), (dict(val=20), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2),
     (dict(n_light_primal=2), -1), (dict(n_light_primal=-1), -1),
-    (dict(n_light_primal=0), -1),                        # dual path needs k > 64
+    (dict(n_light_primal=0, k=32, ld=32), -1),           # dual path needs k > 32
     (dict(n_light_primal=0, k=128, ld=128, reg=0.0), -1),  # ... and regParam > 0
     (dict(n_light_primal=0, k=128, ld=128, implicit=1, yty=8), -1)])  # ... and explicit
 def test_solve_half_argument_errors(over, code):

@@ -255,20 +255,23 @@ def _degree_data(degrees, n_items, seed):
     return u, i, r
 
 
-DUAL_DEGREES = [1, 2, 7, 15, 16, 17, 31, 32, 33, 40, 48, 63, 64, 65, 66, 90, 128, 129]
+DUAL_DEGREES = [1, 2, 7, 15, 16, 17, 31, 32, 33, 40, 48, 63, 64, 65, 66, 90, 96, 97, 128, 129]
 
 
-@pytest.mark.parametrize("rank", [65, 96, 100, 128])
+@pytest.mark.parametrize("rank", [33, 40, 64, 65, 96, 100, 128])
 def test_dual_short_rows_match_primal_and_oracle(rank):
-    """Explicit rows with <= 64 ratings at rank 65-128 go through the n x n dual
-    system (NB = 2 for n <= 32, 4 for n <= 64); the rest through the k x k primal.
-    Both forms vs the fp64 oracle of Spark's k x k normal equations, per row, with
-    the degrees around every class boundary (1, 16/17, 32/33, 64/65)."""
+    """Explicit rows with <= 96 ratings at rank 65-128 go through the n x n dual
+    system (NB = 2 for n <= 32, 4 for n <= 64, 6 for n <= 96), rows with <= 32 ratings
+    at rank 33-64 too (NB = 2, split table of 64 words per row); the rest through the
+    k x k primal.  Both forms vs the fp64 oracle of Spark's k x k normal equations, per
+    row, with the degrees around every class boundary (1, 16/17, 32/33, 64/65, 96/97)."""
     degrees = DUAL_DEGREES * 15
     u, i, r = _degree_data(degrees, 400, seed=rank)
     core = _core(u, i, r, chunk=256)
     ub = core.user_block
     assert ub.n_short == sum(d <= E.DUAL_MAX_RATINGS for d in degrees)
+    assert ub.n_short64 == sum(d <= E.DUAL_MAX_RATINGS_64 for d in degrees)
+    assert ub.n_dual(rank) == (ub.n_short if rank > 64 else ub.n_short64)
     core.init_factors(rank, seed=3)
     g = torch.Generator(device=DEV)
     g.manual_seed(rank)

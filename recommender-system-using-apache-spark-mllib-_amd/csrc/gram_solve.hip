@@ -696,6 +696,68 @@ __device__ __forceinline__ void gram_accumulate_pre(
   }
 }
 
+// Two steps of gathers in flight (W1 explicit light rows and chunks, one wave per
+// SIMD: a step's MFMAs alone do not cover an HBM gather latency).  Register sets
+// s0 / s1 hold steps t+1 and t+2 while step t's operands are formed; the rating
+// indices are staged in LDS one block further ahead, in two block slots.
+template <class TS>
+__device__ __forceinline__ void gram_accumulate_pre2(
+    const int32_t* __restrict__ col, const float* __restrict__ val, int64_t pb, int64_t pe,
+    const uint32_t* __restrict__ Ysp, uint32_t kp, int zero_row, float sr, int d0,
+    floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA], int* __restrict__ st) {
+  const int lane = threadIdx.x & 63, m = lane & 15;
+  // slot b % 2: 64 column indices then 64 split rating words
+  if (pe <= pb) return;
+  const uint32_t rsel = m == 0 ? 0x05040100u : (m == 1 ? 0x07060302u : 0x0C0C0C0Cu);
+  const uint32_t* base = Ysp + d0;
+  auto load_idx = [&](int64_t b, int& ci, float& rv) {
+    ci = zero_row;
+    rv = 0.f;
+    if (b + lane < pe) {
+      ci = col[b + lane];
+      rv = val[b + lane];
+    }
+  };
+  auto stage = [&](int slot, int ci, float rv) {
+    st[128 * slot + lane] = ci;
+    reinterpret_cast<uint32_t*>(st + 128 * slot + 64)[lane] = split_word(sr * rv);
+    wave_lds_sync();
+  };
+  auto issue = [&](PreStep<TS::NC>& s, int step) {
+    const int slot = (step >> 1) & 1;
+    pre_issue<TS>(s, st + 128 * slot, reinterpret_cast<const uint32_t*>(st + 128 * slot + 64),
+                  step & 1, base, kp);
+  };
+  const int nsteps = (int)((pe - pb + 31) >> 5);
+  int ci0, ci1, ci_n;
+  float rv0, rv1, rv_n;
+  load_idx(pb, ci0, rv0);
+  load_idx(pb + 64, ci1, rv1);
+  load_idx(pb + 128, ci_n, rv_n);
+  stage(0, ci0, rv0);
+  stage(1, ci1, rv1);
+  PreStep<TS::NC> s0, s1;
+  issue(s0, 0);
+  issue(s1, 1);
+  // step t: operands from s[t % 2]; that set then loads step t + 2 (block (t >> 1) + 1);
+  // after an odd step the slot of block t >> 1 (fully issued) takes block (t >> 1) + 2
+  auto body = [&](PreStep<TS::NC>& s, int t) {
+    uint32_t hi[TS::NC][4], lo[TS::NC][4], rb[4];
+    pre_operands<TS>(s, rsel, hi, lo, rb);
+    pin_operands<TS>(hi, lo, rb);
+    if (t & 1) {
+      stage((t >> 1) & 1, ci_n, rv_n);
+      load_idx(pb + 64 * (int64_t)((t >> 1) + 3), ci_n, rv_n);
+    }
+    issue(s, t + 2);  // past the last step: the zero row's words (never consumed)
+    pre_mfma<TS>(hi, lo, rb, acc, accb);
+  };
+  for (int t = 0; t < nsteps; t += 2) {
+    body(s0, t);
+    if (t + 1 < nsteps) body(s1, t + 1);
+  }
+}
+
 // rhs from the pre path's tiles: b[i*CN + gcol(c)] = C[i][0] + C[i][1] of
 // accb[c], returned in the layout of the split path's partials (lane (0, m)
 // holds dim m*CN + gcol(c), lanes with q > 0 hold 0), times `scale`.
@@ -1766,6 +1828,8 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
 // merge is done in fp64 before the single rounding.
 // ---------------------------------------------------------------------------
 constexpr int kW1NT = 36;
+// Explicit W1 Gram with two gather steps in flight (gram_accumulate_pre2).
+constexpr bool kW1Prefetch2 = true;
 constexpr int kW1Slot = (kW1NT * 4 + kW1NB + 1) * 64;  // floats per chunk partial
 constexpr int kW1YtyC = kW1NT * 4 * 64;               // floats of the C-layout YtY table
 
@@ -1886,9 +1950,14 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     floatx4 accb[CN];
 #pragma unroll
     for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-    gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
-                                       ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
-                                       reinterpret_cast<int*>(smem));
+    if constexpr (kW1Prefetch2)
+      gram_accumulate_pre2<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
+                                          ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
+                                          reinterpret_cast<int*>(smem));
+    else
+      gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
+                                         ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
+                                         reinterpret_cast<int*>(smem));
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
   }
   if (chunk >= 0) {

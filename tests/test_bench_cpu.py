@@ -1,0 +1,70 @@
+"""CPU checks of bench.py's roofline bookkeeping (no GPU): the per-phase kernel parts of a
+half-sweep, the counter lookup by workload / kernel / grid, the combination of several
+kernels' counters in one launch-1 phase, and the top-k kernel / grid naming that
+must match csrc/topk.hip's launch choice."""
+import importlib.util
+import os
+from types import SimpleNamespace
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _block(n_light, n_chunks, n_short, n_short64):
+    blk = SimpleNamespace(n_light=n_light, n_chunks=n_chunks, n_short=n_short, n_short64=n_short64)
+    blk.n_dual = lambda rank: n_short if rank > 64 else (n_short64 if rank > 32 else 0)
+    return blk
+
+
+def test_launch1_parts_name_the_dual_kernel(bench):
+    b = _block(1000, 10, 600, 200)
+    assert bench._launch1_parts(b, 128, False) == [
+        ("gram_solve_w1_kernel<false>", 64 * (10 + 400)), ("gram_solve_dual_kernel<128>", 64 * 600)]
+    assert bench._launch1_parts(b, 64, False) == [
+        ("gram_solve_kernel<4,false>", 64 * (10 + 800)), ("gram_solve_dual_kernel<64>", 64 * 200)]
+    assert bench._launch1_parts(b, 128, True) == [("gram_solve_w1_kernel<true>", 64 * 1010)]
+    assert bench._launch1_parts(b, 16, False) == [("gram_solve_kernel<1,false>", 64 * 1010)]
+
+
+def test_phase_counters_combine_by_grid(bench, monkeypatch):
+    doc = {"format": 2, "workloads": {"w": {
+        "gram_solve_w1_kernel<false>": {"by_grid": {"640": {
+            "fetch_bytes_x2": 4e9, "write_bytes": 1e8, "pmc_run_avg_ns": 3e6, "trace_avg_ns": 3e6,
+            "mfma_busy_frac": 0.4, "valu_busy_frac": 0.2, "mfma_flop_f16": 1e12}}},
+        "gram_solve_dual_kernel<128>": {"by_grid": {"128": {
+            "fetch_bytes_x2": 2e9, "write_bytes": 1e8, "pmc_run_avg_ns": 1e6, "trace_avg_ns": 1e6,
+            "mfma_busy_frac": 0.2, "valu_busy_frac": 0.6, "mfma_flop_f16": 2e11}}}}}}
+    monkeypatch.setattr(bench, "_pmc_doc", lambda: doc)
+    parts = [("gram_solve_w1_kernel<false>", 640), ("gram_solve_dual_kernel<128>", 128)]
+    c = bench._combine_pmc("w", parts)
+    assert c["fetch_bytes_x2"] == 6e9 and c["trace_avg_ns"] == 4e6
+    assert c["mfma_busy_frac"] == pytest.approx((0.4 * 3 + 0.2 * 1) / 4)
+    assert bench._combine_pmc("w", parts + [("missing", 1)]) is None
+    assert bench._combine_pmc("other", parts) is None
+    r = bench.roofline("w", "k", {"user": {"ms": 4.0, "nnz": 10 ** 6, "rows": 1000, "parts": parts}},
+                       128, False)
+    u = r["launches"]["user"]
+    assert u["rocprof_ms"] == pytest.approx(4.0)
+    assert u["mfma_issued_flops_pmc"] == pytest.approx(1.2e12)
+    assert r["traffic"] == pytest.approx(6.2e9)
+    assert r["frac_rocprof"] == pytest.approx(r["frac"])  # same duration here
+
+
+@pytest.mark.parametrize("k,top,n_q,kern,grid", [
+    (128, 10, 10_000_000, "topk_split_kernel<4,2,12,0>", 39063 * 512),
+    (128, 100, 10_000_000, "topk_split_kernel<4,1,100,0>", 78125 * 512),
+    (64, 10, 162_541, "topk_split_kernel<2,1,12,0>", 1270 * 512),
+    (128, 10, 262_144, "topk_split_kernel<4,2,12,0>", 1024 * 512),
+    (128, 10, 262_143, "topk_split_kernel<4,1,12,0>", 2048 * 512),
+    (32, 20, 1000, "topk_split_kernel<1,1,32,0>", 8 * 512)])
+def test_topk_variant_matches_launch_choice(bench, k, top, n_q, kern, grid):
+    assert bench.topk_variant(k, top, n_q) == (kern, grid)

@@ -25,19 +25,24 @@ Secondary objects on the same line (the other BASELINE configs, each at full siz
             factors over ALL 10M users x all 1M items (split over the ranks by user
             range), recs/s = 10M / time.
 
-Every workload carries a roofline of its dominant kernel: algorithmic bytes and
-issued MFMA flops per launch over HIP-event launch times measured on the
-launching stream (`frac`), the same over the rocprofv3 kernel-trace average
-(`frac_rocprof`), and the PMC traffic / busy fractions / limiter of that
-workload's own profiled launches (profiles/pmc_summary.json, keyed by workload,
-kernel and grid size).  `cpu_baseline`: the C port of Spark's per-row dspr +
-dppsv arithmetic (oracle/als_oracle.c) on the host cores, bounded sample, with
-the Spark probe (java / pyspark) recorded.  `--only c1|c2|c3|c4` runs a single
-workload (profiling passes).
+Every workload carries a roofline of its dominant kernel — ONE kernel: the primal
+gram + solve launch of each half-sweep (ALS_PHASE_LAUNCH1), timed alone with HIP
+events on the launching stream; the dual-path launch of the short rows
+(ALS_PHASE_DUAL) is timed and reported beside it (`dual`).  `frac` = algorithmic
+bytes per launch / event time / 8 TB/s; the same over the rocprofv3 kernel-trace
+average (`frac_rocprof`); the PMC traffic / counter DRAM fraction / busy fractions
+/ limiter of that workload's own profiled launches (profiles/pmc_summary.json,
+keyed by workload, kernel and grid size).  `cpu_baseline`: the C port of Spark's
+per-row dspr + dppsv arithmetic (oracle/als_oracle.c) on every host core in this
+process's affinity set, bounded sample, with the Spark probe (java / pyspark)
+recorded.  `--only c1|c2|c3|c4` runs a single workload (profiling passes).
+The line records the product library it timed (path + sha256); bench.py refuses
+ALS_HIP_LIB (a dev-build override of the library path).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -45,6 +50,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+if os.environ.get("ALS_HIP_LIB"):
+    sys.exit("bench.py times the in-tree product library only: unset ALS_HIP_LIB "
+             f"(= {os.environ['ALS_HIP_LIB']})")
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -122,6 +130,15 @@ def load_pmc(workload: str, kernel: str, grid=None):
     if grid is not None:
         return ent.get("by_grid", {}).get(str(int(grid)))
     return ent
+
+
+def library_record() -> dict:
+    """The libals_hip.so this process timed: path and sha256 of its bytes."""
+    from als_mi355x import _lib
+    path = os.path.realpath(_lib.LIB_PATH)
+    with open(path, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    return {"path": os.path.relpath(path, ROOT), "sha256": sha, "abi": _lib.ABI_VERSION}
 
 
 def _pmc_view(pmc, t_s):
@@ -232,7 +249,14 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
     busy = {k_: x / te for k_, x in busy_w.items()} if busy_w else {}
     if busy:
         out["limiter"] = max(busy, key=busy.get)
+        out["limiter_busy"] = busy[out["limiter"]]
         out["limiter_fracs"] = busy
+    if have_traffic and traffic > 0:
+        # counter-measured DRAM-side bytes (PMC FETCH_SIZE x 2 + WRITE_SIZE) over the same
+        # event time: what actually crossed the memory side (the algorithmic bytes are
+        # largely served from the Infinity Cache at the ML-25M shape)
+        out["counter_dram_gbs"] = traffic / te / 1e9
+        out["counter_dram_frac"] = traffic / te / 1e9 / PEAK_HBM_GBS
     # bound (contract: hbm | mfma): the larger counter-measured fraction of the two when
     # the counters exist, else the larger algorithmic view
     if "hbm" in busy and "mfma" in busy:
@@ -316,17 +340,28 @@ def _probe_spark():
     return {"java": java, "pyspark": pys}
 
 
+def _cgroup_cpu_max():
+    """The cgroup v2 CPU quota of this process ("max 100000" = none), if readable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            return f.read().strip()
+    except Exception:
+        return None
+
+
 def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.0,
                  implicit: bool = False, alpha: float = 1.0):
     """Time the C port (oracle/als_oracle.c, OpenMP) on a bounded prefix of rows of each side;
     extrapolate to ratings/s of a full iteration."""
     import numpy as np
     from oracle import c_oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    # every core this process may run on (SURVEY §8d: "N = all host cores"), passed
+    # explicitly to the OpenMP port (OMP_NUM_THREADS is left as the host set it)
     try:
         affinity = len(os.sched_getaffinity(0))
     except Exception:
         affinity = None
+    threads = affinity or os.cpu_count()
     U = core.U[:, :rank].contiguous().cpu().numpy()
     V = core.V[:, :rank].contiguous().cpu().numpy()
     total_t = 0.0
@@ -354,6 +389,8 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
     probe = _probe_spark()
     return {"value": core.nnz / total_t, "unit": "ratings/s", "cores": threads, "kind": "port",
             "host_cores": os.cpu_count(), "affinity_cores": affinity, "spark_probe": probe,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+            "cgroup_cpu_max": _cgroup_cpu_max(),
             "sample": "oracle/als_oracle.c (Spark dspr+dppsv restated, fp64, OpenMP, "
                       f"{threads} threads) on a row prefix of each side; "
                       + "; ".join(sample_desc)
@@ -377,14 +414,21 @@ def _timed_topk(Q, n_q, V, n_v, k, top):
 
 
 def _half_sweep_timed(core, block, Y, X, k, reg, imp, alpha, yty, ev=None):
-    """solve_half in its phases, launch 1 bracketed by events (ev = (start, end))."""
-    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, 12)
+    """solve_half in its phases (the normal call's order), the primal launch and the
+    dual launch each bracketed by events on the launching stream (ev = 3 events)."""
+    P = E  # phase bits: engine.PHASE_*
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
+                 P.PHASE_PREP | P.PHASE_RSCALE)
     if ev is not None:
         ev[0].record()
-    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, 1)
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, P.PHASE_LAUNCH1)
     if ev is not None:
         ev[1].record()
-    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, 2)
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, P.PHASE_DUAL)
+    if ev is not None:
+        ev[2].record()
+    E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
+                 P.PHASE_LAUNCH2 | P.PHASE_RESCUE)
 
 
 def _iteration(core, k, reg, imp, alpha, evs=None):
@@ -392,33 +436,62 @@ def _iteration(core, k, reg, imp, alpha, evs=None):
     from items; implicit: YtY of the source side before each half-sweep (computeYtY)."""
     yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
     _half_sweep_timed(core, core.item_block, core.U, core.V, k, reg, imp, alpha, yty,
-                      evs[0:2] if evs else None)
+                      evs[0:3] if evs else None)
     yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
     _half_sweep_timed(core, core.user_block, core.V, core.U, k, reg, imp, alpha, yty,
-                      evs[2:4] if evs else None)
+                      evs[3:6] if evs else None)
 
 
-def _launch1_parts(block, k: int, imp: bool):
-    """Kernels of launch-1 phase of a half-sweep, as als_solve_half launches them:
-    [(kernel, grid threads)] (engine.solve_half: the dual kernel for the short explicit
-    rows at 32 < k <= 128)."""
+def _n_dual(block, k: int, imp: bool, reg: float = 0.1) -> int:
+    return 0 if (imp or reg <= 0) else block.n_dual(k)
+
+
+def dual_kernel(k: int) -> str:
+    return f"gram_solve_dual_kernel<{128 if k > 64 else 64}>"
+
+
+def _launch1_parts(block, k: int, imp: bool, reg: float = 0.1):
+    """Kernels als_solve_half launches for a half-sweep's light rows: [(kernel, grid
+    threads)] — the primal launch (ALS_PHASE_LAUNCH1: chunk tasks + primal light rows),
+    then, when there are dual rows, the dual launch (ALS_PHASE_DUAL)."""
     kern = dominant_kernel(k, imp)
-    n_dual = 0 if imp else block.n_dual(k)
+    n_dual = _n_dual(block, k, imp, reg)
     parts = [(kern, 64 * (block.n_chunks + block.n_light - n_dual))]
     if n_dual > 0:
-        parts.append((f"gram_solve_dual_kernel<{128 if k > 64 else 64}>", 64 * n_dual))
+        parts.append((dual_kernel(k), 64 * n_dual))
     return parts
+
+
+def dual_view(workload: str, k: int, blocks: dict, ms: dict, reg: float):
+    """The dual launch of each half-sweep (explicit short rows): event time, algorithmic
+    bytes (each rating's factor row + index + rating, each row's output) and HBM
+    fraction, plus that kernel's PMC view when profiled."""
+    out = {"kernel": dual_kernel(k), "launches": {}}
+    for name, blk in blocks.items():
+        nd = _n_dual(blk, k, False, reg)
+        if nd == 0:
+            continue
+        b = gather_bytes(blk.dual_nnz(k), nd, k)
+        t = ms[name] * 1e-3
+        ent = {"rows": nd, "nnz": blk.dual_nnz(k), "event_ms": ms[name], "algorithmic_bytes": b,
+               "hbm_frac": b / t / 1e9 / PEAK_HBM_GBS}
+        pv = _pmc_view(load_pmc(workload, dual_kernel(k), 64 * nd), t)
+        if pv:
+            ent["pmc"] = pv
+        out["launches"][name] = ent
+    return out if out["launches"] else None
 
 
 def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
     """warmup + `steps` timed iterations from the seeded start; per-iteration wall time
-    and the event times of launch 1 of each half-sweep -> (ms_per_iter, roofline)."""
+    and the event times of the primal and dual launches of each half-sweep
+    -> (ms_per_iter, roofline of the primal kernel, dual view)."""
     core.init_factors(k, seed=5)
     core.status.zero_()
     for _ in range(warmup):
         _iteration(core, k, reg, imp, alpha)
     torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(steps)]
     t0 = time.perf_counter()
     for s in range(steps):
         _iteration(core, k, reg, imp, alpha, evs[s])
@@ -426,21 +499,24 @@ def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
     dt = (time.perf_counter() - t0) / steps
     core.check_status()
     ib, ub = core.item_block, core.user_block
-    launches = {
-        "item": {"ms": sum(e[0].elapsed_time(e[1]) for e in evs) / steps, "nnz": ib.nnz,
-                 "rows": ib.n_light, "parts": _launch1_parts(ib, k, imp)},
-        "user": {"ms": sum(e[2].elapsed_time(e[3]) for e in evs) / steps, "nnz": ub.nnz,
-                 "rows": ub.n_light, "parts": _launch1_parts(ub, k, imp)}}
-    kern = dominant_kernel(k, imp)
-    if any(len(L["parts"]) > 1 for L in launches.values()):
-        kern += " + " + next(p[0] for L in launches.values() for p in L["parts"][1:])
-    return 1e3 * dt, roofline(workload, kern, launches, k, imp)
+
+    def avg(a, b):
+        return sum(e[a].elapsed_time(e[b]) for e in evs) / steps
+    launches = {}
+    for name, blk, o in (("item", ib, 0), ("user", ub, 3)):
+        nd = _n_dual(blk, k, imp, reg)
+        launches[name] = {"ms": avg(o, o + 1), "nnz": blk.nnz - (blk.dual_nnz(k) if nd else 0),
+                          "rows": blk.n_light - nd, "parts": _launch1_parts(blk, k, imp, reg)[:1]}
+    roof = roofline(workload, dominant_kernel(k, imp), launches, k, imp)
+    dual = None if imp else dual_view(workload, k, {"item": ib, "user": ub},
+                                      {"item": avg(1, 2), "user": avg(4, 5)}, reg)
+    return 1e3 * dt, roof, dual
 
 
 def configs2(core, args):
     """BASELINE configs[2]: the ML-25M shape, implicitPrefs=True alpha=40, rank 128."""
     k, alpha = 128, 40.0
-    ms, roof = timed_fit(core, "configs2", k, args.reg, True, alpha, args.steps, args.warmup)
+    ms, roof, _ = timed_fit(core, "configs2", k, args.reg, True, alpha, args.steps, args.warmup)
     return {"workload": "ml25m implicit alpha=40 ALS rank 128 (BASELINE configs[2]), 1 GPU",
             "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz, "rank": k,
             "alpha": alpha, "ratings_per_s": core.nnz / (ms * 1e-3), "ms_per_iter": ms,
@@ -463,12 +539,12 @@ def big_single(args, dev, want_c3=True, want_c4=True):
     steps = max(1, min(args.steps, args.big_steps))
     c3 = c4 = None
     if want_c3:
-        ms, roof = timed_fit(core, "configs3", k, args.reg, False, 1.0, steps, 1)
+        ms, roof, dual = timed_fit(core, "configs3", k, args.reg, False, 1.0, steps, 1)
         c3 = {"workload": "big1b explicit ALS rank 128 (BASELINE configs[3]), 1 GPU",
               "n_users": core.n_users, "n_items": core.n_items, "nnz": core.nnz, "rank": k,
               "ratings_per_s": core.nnz / (ms * 1e-3), "ms_per_iter": ms, "steps": steps,
               "warmup": 1, "datagen_s": t_gen, "build_s": t_build, "scaling": "strong",
-              "n_gpus": 1, "roofline": roof,
+              "n_gpus": 1, "roofline": roof, "dual": dual,
               "schedule": {"item": [core.item_block.n_light, core.item_block.n_heavy,
                                     core.item_block.n_chunks],
                            "user": [core.user_block.n_light, core.user_block.n_heavy,
@@ -517,7 +593,8 @@ def run_single(args):
     k = args.rank
     imp, alpha = args.implicit, args.alpha
     wl = "configs2" if (imp and k == 128) else "configs1"
-    ms_per_step, roof = timed_fit(core, wl, k, args.reg, imp, alpha, args.steps, args.warmup)
+    ms_per_step, roof, dual = timed_fit(core, wl, k, args.reg, imp, alpha, args.steps,
+                                        args.warmup)
     value = core.nnz / (ms_per_step * 1e-3)
     ib, ub = core.item_block, core.user_block
     # top-10 recommendations for all users (K5)
@@ -543,6 +620,8 @@ def run_single(args):
                    "rank": k, "regParam": args.reg, "implicitPrefs": imp, "alpha": alpha,
                    "parallelism": "dp1"},
         "roofline": roof,
+        "dual": dual,
+        "library": library_record(),
         "topk10_recs_per_s": core.n_users / (topk_ms * 1e-3),
         "topk10_ms": topk_ms,
         "topk_roofline": topk_roofline("configs1", core.n_users, core.n_items, k, topk_ms, 10),
@@ -688,6 +767,7 @@ def run_distributed(args):
                        "rank": k, "regParam": args.reg, "parallelism": f"dp{world}"},
             "roofline": None,
             "cpu_baseline": None,
+            "library": library_record(),
         }
     del sh
     torch.cuda.empty_cache()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 4
+#define ALS_ABI_VERSION 5
 
 #define ALS_OK 0
 #define ALS_EINVAL (-1)   /* bad argument (shape, null pointer, rank) */
@@ -110,14 +110,23 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * fp64 k_pad x k_pad Gram from als_yty.  status_dev: device int32, set to
  * (row+1) of a row whose Cholesky pivot was not positive (0 = all rows ok;
  * Spark raises from dppsv in that case).  ws: 16-byte aligned.
- * phases: bit 2 = Y_src prep (max |Y_src|; explicit: the split table), bit 3 =
- * rating scale (max |rating| of this block), bit 0 = launch 1 (heavy-row chunk
- * partials + fused light-row gram/solve), bit 1 = launch 2 (heavy-row reduce +
- * solve); 15 = all (the normal call).  They run in the order 2, 3, 0, 1; split
- * across calls, issue them in that order on one stream with the same
- * workspace.  Blocks that share Y_src (row chunks of one half-sweep) may share
- * one bit-2 prep: it sits at a fixed workspace offset (size the workspace for
- * the largest n_chunks).
+ * phases (ALS_PHASE_* bits below; ALS_PHASE_ALL = the normal call): PREP = Y_src
+ * prep (max |Y_src|; explicit: the split table), RSCALE = rating scale (max
+ * |rating| of this block), LAUNCH1 = heavy-row chunk partials + fused primal
+ * light-row gram/solve, DUAL = the dual-path light rows (see n_light_primal),
+ * LAUNCH2 = heavy-row reduce + solve, RESCUE = re-solve of the rows that missed
+ * the split window (below).  They run in the order PREP, RSCALE, LAUNCH1, DUAL,
+ * LAUNCH2, RESCUE; split across calls, issue them in that order on one stream
+ * with the same workspace (a call holding PREP, RSCALE or LAUNCH1 starts a new
+ * rescue list).  Blocks that share Y_src (row chunks of one half-sweep) may share
+ * one PREP: it sits at a fixed workspace offset (size the workspace for the
+ * largest n_chunks and n_rows).
+ * Split window (explicit): the Gram/rhs split uses one power-of-two scale per
+ * launch, so a row whose own factor rows (or ratings) all sit more than ~2^18
+ * below the launch maxima would lose precision in the f16 lo halves.  Such a row
+ * is detected in its task (max diagonal of its Gram / max |rating| against the
+ * window) and re-solved in the RESCUE launch with a scale of its own (fp32 rows
+ * split in registers, fp32 rhs), so the 1e-4 bar holds for any magnitude spread.
  * n_light_primal (0 <= n_light_primal <= n_light): the first n_light_primal light
  * rows are solved on the k x k normal equations above; the remaining light rows
  * (the tail of the longest-first light list) must have <= 96 ratings (64 < k <= 128)
@@ -126,7 +135,15 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * Y^T (Y Y^T + lambda n I)^-1 r), allowed for explicit feedback, 32 < k <= 128,
  * reg > 0 only (a longer row there is reported through status_dev).
  * n_light_primal = n_light keeps every row on the primal path. */
-size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src);
+#define ALS_PHASE_LAUNCH1 1
+#define ALS_PHASE_LAUNCH2 2
+#define ALS_PHASE_PREP 4
+#define ALS_PHASE_RSCALE 8
+#define ALS_PHASE_DUAL 16
+#define ALS_PHASE_RESCUE 32
+#define ALS_PHASE_ALL 63
+/* n_rows: rows of the block (n_light + n_heavy; the largest block when shared). */
+size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows);
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light, int32_t n_light_primal,
                    const int32_t* heavy_rows, const int32_t* heavy_slot_begin, int32_t n_heavy,

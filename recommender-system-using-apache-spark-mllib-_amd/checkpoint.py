@@ -133,6 +133,11 @@ def save(dirpath: str, iteration: int, rank: int, reg: float, implicit: bool, al
         if name != gen and (name.startswith(_GEN) or (name.startswith("." + _GEN)
                                                        and name.endswith(".tmp"))):
             shutil.rmtree(os.path.join(dirpath, name), ignore_errors=True)
+    for name in (IDS, FACTORS, IIDS, IFACTORS):  # a format-1 layout's top-level files
+        try:
+            os.remove(os.path.join(dirpath, name))
+        except FileNotFoundError:
+            pass
 
 
 def load(dirpath: str) -> Optional[State]:
@@ -195,6 +200,13 @@ def resume_point(dirpath: Optional[str], resume, engine, rank: int, reg: float, 
         return 0, None, None
     ids = engine.user_factor_ids().cpu().numpy()
     fp = fingerprint if fingerprint is not None else engine.fingerprint()
+    if resume is not True and init is not None and st.init is None:
+        # a format-1 (round-2) checkpoint records no initialisation, so "auto" cannot
+        # prove it belongs to this fit (a checkpoint must never change the model)
+        import warnings
+        warnings.warn(f"{dirpath}: checkpoint without an initialisation record (format 1); "
+                      "resume='auto' does not use it (pass resume=True to continue from it)")
+        return 0, None, None
     why = mismatch(st, rank, reg, implicit, alpha, fp, ids,
                    init=None if resume is True else init)
     if why is None and st.iteration > max_iter:
@@ -221,17 +233,21 @@ def resume_point_agreed(dirpath: Optional[str], resume, engine, rank: int, reg: 
     proc = dist.get_rank(group)
     start, U, V, err = 0, None, None, None
     if proc == 0:
+        # any failure (a mismatch, a missing or unreadable generation directory, a
+        # malformed JSON) is broadcast, so every rank raises instead of waiting
         try:
             start, U, V = resume_point(dirpath, resume, engine, rank, reg, implicit, alpha,
                                        max_iter, init, fingerprint=fp)
-        except ValueError as e:
-            err = str(e)
+        except Exception as e:  # noqa: BLE001 - re-raised on every rank below
+            err = (type(e).__name__, str(e))
     head = [start, V is not None, err]
     src = dist.get_global_rank(group, 0) if group is not None else 0
     dist.broadcast_object_list(head, src=src, group=group)
     start, has_v, err = head
     if err is not None:
-        raise ValueError(err)
+        kind, msg = err
+        raise (ValueError if kind == "ValueError" else RuntimeError)(
+            msg if kind == "ValueError" else f"checkpoint in {dirpath} unreadable: {kind}: {msg}")
     if start == 0 and not has_v:
         return 0, None, None
 

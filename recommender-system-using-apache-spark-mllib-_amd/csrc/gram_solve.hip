@@ -50,6 +50,8 @@ namespace als {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
+constexpr int kRescueGrid = 256;     // waves walking the rescue list (rescue_kernel)
+constexpr int kRescueChunk = 2048;   // fp32 accumulation span of a rescued row
 constexpr int kMaxRank = 128;
 
 template <int CN>
@@ -653,7 +655,7 @@ template <class TS>
 __device__ __forceinline__ void gram_accumulate_pre(
     const int32_t* __restrict__ col, const float* __restrict__ val, int64_t pb, int64_t pe,
     const uint32_t* __restrict__ Ysp, uint32_t kp, int zero_row, float sr, int d0,
-    floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA], int* __restrict__ st) {
+    floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA], int* __restrict__ st, float& rmax) {
   const int lane = threadIdx.x & 63, m = lane & 15;
   int* st_c = st;
   uint32_t* st_r = reinterpret_cast<uint32_t*>(st + 64);
@@ -671,6 +673,7 @@ __device__ __forceinline__ void gram_accumulate_pre(
   auto stage = [&](int ci, float rv) {
     st_c[lane] = ci;
     st_r[lane] = split_word(sr * rv);
+    rmax = fmaxf(rmax, __builtin_fabsf(rv));
     wave_lds_sync();
   };
   const int nsteps = (int)((pe - pb + 31) >> 5);
@@ -704,7 +707,7 @@ template <class TS>
 __device__ __forceinline__ void gram_accumulate_pre2(
     const int32_t* __restrict__ col, const float* __restrict__ val, int64_t pb, int64_t pe,
     const uint32_t* __restrict__ Ysp, uint32_t kp, int zero_row, float sr, int d0,
-    floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA], int* __restrict__ st) {
+    floatx4 (&acc)[TS::N], floatx4 (&accb)[TS::NRA], int* __restrict__ st, float& rmax) {
   const int lane = threadIdx.x & 63, m = lane & 15;
   // slot b % 2: 64 column indices then 64 split rating words
   if (pe <= pb) return;
@@ -721,6 +724,7 @@ __device__ __forceinline__ void gram_accumulate_pre2(
   auto stage = [&](int slot, int ci, float rv) {
     st[128 * slot + lane] = ci;
     reinterpret_cast<uint32_t*>(st + 128 * slot + 64)[lane] = split_word(sr * rv);
+    rmax = fmaxf(rmax, __builtin_fabsf(rv));
     wave_lds_sync();
   };
   auto issue = [&](PreStep<TS::NC>& s, int step) {
@@ -1321,6 +1325,50 @@ __device__ __forceinline__ float absmax4(const floatx4& x) {
                fmaxf(__builtin_fabsf(x[2]), __builtin_fabsf(x[3])));
 }
 
+// ---------------------------------------------------------------------------
+// Split window guard.  The explicit Gram and rhs use ONE power-of-two scale per
+// launch (max |Y_src| -> [2^14, 2^15), max |rating| likewise), so the f16 lo half
+// of an operand t goes subnormal once |t| < 2^-3 and its relative precision then
+// degrades towards 2^-24 / |t|.  A row whose own operands all sit that far below
+// the launch maxima (a user-supplied U0, a loaded model, ratings spanning many
+// decades) would silently lose precision.  Each explicit task therefore checks
+// its scaled operands against a window T = 2^-4 (precision of its largest
+// operand >= 2^-20, 16x inside the fp32-grade split):
+//   max diag(G) < n T^2  (covers every row whose largest |t| < T: diag <= n max t^2)
+//   or 0 < max |r| < T   (the row's ratings, scaled by the launch's rating scale).
+// A row that misses the window is not solved here: it is appended to the rescue
+// list and re-solved by rescue_kernel with a scale of its own (fp32 rows split in
+// registers after a per-row power of two, rhs in fp32).  Implicit rows need no
+// guard: their A includes YtY (>= the largest row's square) and b is fp32.
+// ---------------------------------------------------------------------------
+constexpr float kWindowT = 0.0625f;  // 2^-4, in scaled units (launch max in [2^14, 2^15))
+
+// Largest diagonal entry of an upper-tile set in the MFMA C layout (this lane's).
+template <int CN>
+__device__ __forceinline__ float diag_max_lane(const floatx4 (&A)[CN * (CN + 1) / 2]) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  float d = 0.f;
+#pragma unroll
+  for (int c = 0; c < CN; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * q + r == m) d = fmaxf(d, A[tile_index(CN, c, c)][r]);
+  return d;
+}
+
+// Wave-uniform: do the scaled operands of a task with n terms miss the window?
+__device__ __forceinline__ bool window_miss(float diag_lane, float n_terms, float rmax_lane) {
+  const float d = wave_max(diag_lane), r = wave_max(rmax_lane);
+  return (d > 0.f && d < n_terms * (kWindowT * kWindowT)) || (r > 0.f && r < kWindowT);
+}
+
+// Append `row` to the rescue list (one lane; each row is appended at most once per
+// half-sweep, so the list never exceeds the rows of the block).
+__device__ __forceinline__ void rescue_append(unsigned* __restrict__ cnt, int32_t* __restrict__ list,
+                                              int row) {
+  if ((threadIdx.x & 63) == 0) list[atomicAdd(cnt, 1u)] = row;
+}
+
 // [hi | lo] f16 halves of s * x (s a power of two): hi = f16(s x) and
 // lo = f16(s x - hi), each one v_fma_mix (the fp32 fma inside is exact).
 __device__ __forceinline__ half8v split_hl(const floatx4& x, float s) {
@@ -1614,7 +1662,7 @@ struct Slot {
 
 template <int N, int NRA, class AccT>
 __device__ __forceinline__ void store_slot(double* __restrict__ slot, const AccT (&tot)[N][4],
-                                           const AccT (&bt)[NRA], int npos) {
+                                           const AccT (&bt)[NRA], float npos) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int t = 0; t < N; ++t)
@@ -1674,7 +1722,7 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const float* __restrict__ Y, float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status,
     const float* __restrict__ scal, const uint32_t* __restrict__ Ysp, int32_t kp,
-    int32_t zero_row) {
+    int32_t zero_row, unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
   constexpr int NT = Cfg<CN>::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   floatx4 acc[NT];
@@ -1697,6 +1745,7 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     pe = row_ptr[row + 1];
   }
   float inv2;
+  float rmax = 0.f;  // explicit: this lane's max |rating| (split window guard)
   if constexpr (IMPLICIT) {
     const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
     inv2 = ldexpf(1.f, -2 * e);
@@ -1710,15 +1759,23 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
     gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
                                        ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
-                                       reinterpret_cast<int*>(smem));
+                                       reinterpret_cast<int*>(smem), rmax);
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
+    rmax *= ldexpf(1.f, er);
+    if (chunk < 0 && window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax)) {
+      rescue_append(rescue_cnt, rescue_list, row);
+      return;
+    }
   }
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) tot[t][r] = acc[t][r] * inv2;
   if (chunk >= 0) {
-    store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt, npos);
+    // explicit: the npos entry carries the chunk's scaled max |rating| (launch 2 takes
+    // the max over the chunks for the window guard)
+    store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt,
+                              IMPLICIT ? (float)npos : rmax);
     return;
   }
   __syncthreads();  // staging area is reused by the solve
@@ -1781,7 +1838,8 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
 // Launch 2a (k <= 64): a heavy row's fp64 chunk slots summed element-wise (one
 // thread per slot element, four interleaved partial sums in a fixed order) into its
 // first slot; each thread reads and writes only its own element.
-template <int SLOT>
+// Explicit: the last 64 entries (each chunk's scaled max |rating|) take the max.
+template <int SLOT, bool IMPLICIT>
 __global__ __launch_bounds__(256) void heavy_sum_f64_kernel(const int32_t* __restrict__ slot_begin,
                                                             double* __restrict__ slots) {
   const int h = blockIdx.y;
@@ -1789,6 +1847,12 @@ __global__ __launch_bounds__(256) void heavy_sum_f64_kernel(const int32_t* __res
   if (e >= SLOT) return;
   const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
   if (s1 - s0 <= 1) return;
+  if (!IMPLICIT && e >= SLOT - 64) {
+    double mx = 0.0;
+    for (int s = s0; s < s1; ++s) mx = fmax(mx, slots[(int64_t)s * SLOT + e]);
+    slots[(int64_t)s0 * SLOT + e] = mx;
+    return;
+  }
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   int s = s0;
   for (; s + 4 <= s1; s += 4) {
@@ -1806,7 +1870,8 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
     const int32_t* __restrict__ slot_begin, const double* __restrict__ slots,
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
-    int32_t* __restrict__ status) {
+    int32_t* __restrict__ status, const float* __restrict__ scal,
+    unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
   constexpr int NT = Cfg<CN>::NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int h = blockIdx.x;
@@ -1815,8 +1880,23 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
   // the row's chunk slots were summed into its first slot (heavy_sum_f64_kernel)
-  add_slot<NT, CN>(slots + (int64_t)slot_begin[h] * Cfg<CN>::SLOT, a64, b64, npos);
+  const double* sl = slots + (int64_t)slot_begin[h] * Cfg<CN>::SLOT;
+  add_slot<NT, CN>(sl, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
+  if constexpr (!IMPLICIT) {  // split window guard over the whole row
+    const float s2 = ldexpf(1.f, 2 * split_exponent(scal[0]));
+    float d = 0.f;
+    const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CN; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * q + r == m) d = fmaxf(d, (float)a64[tile_index(CN, c, c)][r] * s2);
+    if (window_miss(d, (float)n_reg, (float)sl[(NT * 4 + CN) * 64 + lane])) {
+      rescue_append(rescue_cnt, rescue_list, row);
+      return;
+    }
+  }
   finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
                                          X + (int64_t)row * ld, ld, row, status);
 }
@@ -1917,7 +1997,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
     int k, float reg, float alpha, const float* __restrict__ ytyC, float* __restrict__ slots,
     int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
-    int32_t kp, int32_t zero_row) {
+    int32_t kp, int32_t zero_row, unsigned* __restrict__ rescue_cnt,
+    int32_t* __restrict__ rescue_list) {
   constexpr int CN = 8, NT = kW1NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
@@ -1941,6 +2022,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     pe = row_ptr[row + 1];
   }
   float inv2;
+  float rmax = 0.f;  // explicit: this lane's max |rating| (split window guard)
   if constexpr (IMPLICIT) {
     const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
     inv2 = ldexpf(1.f, -2 * e);
@@ -1955,12 +2037,17 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     if constexpr (kW1Prefetch2)
       gram_accumulate_pre2<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
                                           ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
-                                          reinterpret_cast<int*>(smem));
+                                          reinterpret_cast<int*>(smem), rmax);
     else
       gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
                                          ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
-                                         reinterpret_cast<int*>(smem));
+                                         reinterpret_cast<int*>(smem), rmax);
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
+    rmax *= ldexpf(1.f, er);
+    if (chunk < 0 && window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax)) {
+      rescue_append(rescue_cnt, rescue_list, row);
+      return;
+    }
   }
   if (chunk >= 0) {
     float* slot = slots + (int64_t)chunk * kW1Slot;
@@ -1970,7 +2057,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
       for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = acc[t][r] * inv2;
 #pragma unroll
     for (int c = 0; c < CN; ++c) slot[(NT * 4 + c) * 64 + lane] = bt[c];
-    slot[(NT * 4 + CN) * 64 + lane] = (float)npos;
+    // explicit: the chunk's scaled max |rating| (launch 2a takes the max over chunks)
+    slot[(NT * 4 + CN) * 64 + lane] = IMPLICIT ? (float)npos : rmax;
     return;
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
@@ -2027,7 +2115,9 @@ template <int NB, int KP>
 __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
                                          const float (&rj)[2], const uint32_t* __restrict__ Ysp,
                                          int ey, float reg, float* __restrict__ xrow, int ld,
-                                         float* __restrict__ lds, int32_t* __restrict__ status) {
+                                         float* __restrict__ lds, int32_t* __restrict__ status,
+                                         unsigned* __restrict__ rescue_cnt,
+                                         int32_t* __restrict__ rescue_list) {
   constexpr int NT = NB * (NB + 1) / 2;
   constexpr int NS = KP / 32;  // k-steps of 32 dims
   typedef FullTiles<NB> TS;
@@ -2082,6 +2172,11 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_h8(lo[a]), hb, acc[t], 0, 0, 0);
     });
   });
+  // split window guard: G_jj = |t_j|^2 <= KP max_d t_jd^2 (ratings are not split here)
+  if (window_miss(diag_max_lane<NB>(acc), (float)KP, 0.f)) {
+    rescue_append(rescue_cnt, rescue_list, row);
+    return;
+  }
   // (2^2ey G + 2^2ey lambda n I) z = 2^2ey r; ratings j >= n: identity rows, rhs 0
   const float inv = ldexpf(1.f, 2 * ey);
   const float lam = (float)((double)reg * (double)n) * inv;
@@ -2162,7 +2257,8 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
     float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
-    const uint32_t* __restrict__ Ysp, int32_t zero_row) {
+    const uint32_t* __restrict__ Ysp, int32_t zero_row, unsigned* __restrict__ rescue_cnt,
+    int32_t* __restrict__ rescue_list) {
   static_assert(KP == 64 || KP == 128, "dual: k_pad 64 or 128");
   constexpr int NMAX = KP == 128 ? kDualMaxRatings : kDualMaxRatings64;
   __shared__ __attribute__((aligned(16))) float lds[W1LdsT<KP == 128 ? 6 : 2>::SIZE];
@@ -2186,14 +2282,17 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     rj[h] = j < n ? val[pb + j] : 0.f;
   }
   if constexpr (KP == 64) {
-    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt, rescue_list);
   } else {
     if (n <= 32)
-      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
+                       rescue_list);
     else if (n <= 64)
-      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
+                       rescue_list);
     else
-      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status);
+      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
+                       rescue_list);
   }
 }
 
@@ -2225,6 +2324,11 @@ __global__ __launch_bounds__(256) void heavy_sum_w1_kernel(const int32_t* __rest
   for (; s < s1; ++s) a0 += (double)slots[(int64_t)s * kW1Slot + e];
   double v = (a0 + a1) + (a2 + a3);
   const int ent = e >> 6;
+  if (!IMPLICIT && ent == NT * 4 + CN) {  // the chunks' scaled max |rating|: max, not sum
+    float mx = 0.f;
+    for (s = s0; s < s1; ++s) mx = fmaxf(mx, slots[(int64_t)s * kW1Slot + e]);
+    v = mx;
+  }
   if (IMPLICIT && ent < NT * 4) {
     const int t = ent >> 2, r = ent & 3, lane = e & 63;
     const int i = (4 * (lane >> 4) + r) * CN + FullTiles<CN>::l1(t);
@@ -2240,7 +2344,9 @@ template <bool IMPLICIT>
 __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
     const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
-    float* __restrict__ X, int ld, int k, float reg, int32_t* __restrict__ status) {
+    float* __restrict__ X, int ld, int k, float reg, int32_t* __restrict__ status,
+    const float* __restrict__ scal, unsigned* __restrict__ rescue_cnt,
+    int32_t* __restrict__ rescue_list) {
   constexpr int CN = 8, NT = kW1NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
@@ -2255,8 +2361,93 @@ __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
   for (int c = 0; c < CN; ++c) bt[c] = sl[(NT * 4 + c) * 64];
   const float npos_f = sl[(NT * 4 + CN) * 64];
   const int64_t n_reg = IMPLICIT ? (int64_t)npos_f : (row_ptr[row + 1] - row_ptr[row]);
+  if constexpr (!IMPLICIT) {  // split window guard over the whole row (npos_f: max |rating|)
+    const float s2 = ldexpf(1.f, 2 * split_exponent(scal[0]));
+    if (window_miss(diag_max_lane<CN>(A) * s2, (float)n_reg, npos_f)) {
+      rescue_append(rescue_cnt, rescue_list, row);
+      return;
+    }
+  }
   w1_finish_and_solve<false>(A, 1.f, bt, n_reg, nullptr, smem, k, reg, X + (int64_t)row * ld, ld,
                              row, status);
+}
+
+// Rescue launch: the rows whose operands missed the split window (window_miss)
+// are re-solved with a scale of their own.  One wavefront per listed row (a grid
+// of a few hundred waves walks the list; an empty list costs one launch): the
+// row's max |y| over its source rows sets a per-row power of two, the fp32 rows
+// are split in registers after it (gram_accumulate_split, the implicit kernels'
+// loop with weight 1), the rhs is accumulated in fp32 on the VALU, fp32 within
+// `chunk` ratings and fp64 across chunks (LDS, lane-private), then the same
+// finish + solve as the primal kernels.  Any row length (heavy rows included).
+template <int CN>
+__global__ __launch_bounds__(64, 1) void rescue_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const float* __restrict__ Y, float* __restrict__ X, int ld,
+    int k, float reg, int32_t* __restrict__ status, const unsigned* __restrict__ rescue_cnt,
+    const int32_t* __restrict__ rescue_list, int chunk) {
+  constexpr int NT = Cfg<CN>::NT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  __shared__ double a64s[NT * 4 * 64];
+  __shared__ double b64s[CN * 64];
+  const int lane = threadIdx.x & 63;
+  const unsigned n_list = *rescue_cnt;
+  for (unsigned it = blockIdx.x; it < n_list; it += gridDim.x) {
+    const int row = rescue_list[it];
+    const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
+    float mx = 0.f;
+    for (int64_t e = pb + lane; e < pe; e += 64) {
+      const float* yr = Y + (int64_t)col[e] * ld;
+      for (int d = 0; d < k; ++d) mx = fmaxf(mx, __builtin_fabsf(yr[d]));
+    }
+    const int ex = split_exponent(wave_max(mx));
+    const double inv2 = ldexp(1.0, -2 * ex);
+    for (int t = 0; t < NT * 4; ++t) a64s[t * 64 + lane] = 0.0;
+    for (int c = 0; c < CN; ++c) b64s[c * 64 + lane] = 0.0;
+    for (int64_t c0 = pb; c0 < pe; c0 += chunk) {
+      const int64_t c1 = c0 + chunk < pe ? c0 + chunk : pe;
+      floatx4 acc[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+      float bf[CN];
+#pragma unroll
+      for (int c = 0; c < CN; ++c) bf[c] = 0.f;
+      int npos = 0;
+      gram_accumulate_split<CN, false>(col, val, c0, c1, Y, ld, k, 0.f, ldexpf(1.f, ex), acc, bf,
+                                       npos, reinterpret_cast<int*>(smem));
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a64s[(t * 4 + r) * 64 + lane] += (double)acc[t][r] * inv2;
+#pragma unroll
+      for (int c = 0; c < CN; ++c) b64s[c * 64 + lane] += (double)bf[c];
+      wave_lds_sync();
+    }
+    float* xrow = X + (int64_t)row * ld;
+    if constexpr (CN <= 2) {
+      double a64[NT][4], bb[CN];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a64[t][r] = a64s[(t * 4 + r) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < CN; ++c) bb[c] = b64s[c * 64 + lane];
+      finish_and_solve<CN, false, double>(a64, bb, pe - pb, smem, k, reg, nullptr, xrow, ld, row,
+                                          status);
+    } else {
+      floatx4 A[NT];
+      float bt[CN];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) A[t][r] = (float)a64s[(t * 4 + r) * 64 + lane];
+#pragma unroll
+      for (int c = 0; c < CN; ++c) bt[c] = (float)b64s[c * 64 + lane];
+      w1_finish_and_solve<false, CN, CN == 8>(A, 1.f, bt, pe - pb, nullptr, smem, k, reg, xrow,
+                                              ld, row, status);
+    }
+    __syncthreads();  // smem reused by the next listed row
+  }
 }
 
 // K2b: YtY partial Grams over row chunks of Y (unweighted, identity gather), fp64.
@@ -2272,7 +2463,7 @@ __global__ __launch_bounds__(64, 2) void yty_partial_kernel(const float* __restr
   const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
   gram_accumulate<CN, false, true, double>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64, b64,
                                            npos);
-  store_slot<NT, CN, double>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, npos);
+  store_slot<NT, CN, double>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, (float)npos);
 }
 
 template <int CN>
@@ -2309,7 +2500,7 @@ __device__ __forceinline__ void wg_yty_partial_task(const float* __restrict__ Y,
   gram_accumulate<kWgNB, false, true, double, TS>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64,
                                                   b64, npos);
   store_slot<TS::N, TS::NRA, double>(slots + (int64_t)blockIdx.x * kWgSlot + R * kWgSub, a64, b64,
-                                     npos);
+                                     (float)npos);
 }
 
 template <int R>
@@ -2415,12 +2606,17 @@ static size_t solve_table_bytes(int32_t k, int64_t n_src) {
   return align_up(sizeof(uint32_t) * (size_t)als_k_pad(k) * (size_t)((n_src > 0 ? n_src : 0) + 1));
 }
 
-size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src) {
-  // 256 B of scale words | split table ((n_src + 1) x k_pad words, explicit) |
-  // partial slots of the heavy-row chunks.  The first two sit at fixed offsets,
-  // so calls over blocks that share Y_src can share one prep (phases).
-  return 256 + ytyc_bytes(k) + solve_table_bytes(k, n_src) +
-         align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
+static size_t slot_bytes(int32_t k, int32_t n_chunks) {
+  return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
+}
+
+size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows) {
+  // 256 B of scale words (max |Y_src|, max |rating|, rescue count) | split table
+  // ((n_src + 1) x k_pad words, explicit) | partial slots of the heavy-row chunks |
+  // rescue list (n_rows).  The first two sit at fixed offsets, so calls over blocks
+  // that share Y_src can share one prep (phases).
+  return 256 + ytyc_bytes(k) + solve_table_bytes(k, n_src) + slot_bytes(k, n_chunks) +
+         align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0));
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -2451,11 +2647,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
               "als_solve_half: val must be 16-byte aligned");
   ALS_REQUIRE(n_src >= 0 && n_src < (int64_t(1) << 31), ALS_EINVAL,
               "als_solve_half: n_src %lld not in [0, 2^31)", (long long)n_src);
-  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks, n_src), ALS_EWORKSPACE,
+  const int32_t n_rows = n_light + n_heavy;
+  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks, n_src, n_rows), ALS_EWORKSPACE,
               "als_solve_half: workspace %zu < %zu", ws_bytes,
-              als_solve_workspace_bytes(k, n_chunks, n_src));
-  ALS_REQUIRE(phases >= 1 && phases <= 15, ALS_EINVAL,
-              "als_solve_half: phases must be in [1, 15]");
+              als_solve_workspace_bytes(k, n_chunks, n_src, n_rows));
+  ALS_REQUIRE(phases >= 1 && phases <= ALS_PHASE_ALL, ALS_EINVAL,
+              "als_solve_half: phases must be in [1, %d]", ALS_PHASE_ALL);
   ALS_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, ALS_EINVAL,
               "als_solve_half: workspace must be 16-byte aligned");
   hipStream_t st = as_stream(stream);
@@ -2466,10 +2663,15 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   uint32_t* Ysp = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k));
   double* slots = reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k) +
                                             solve_table_bytes(k, n_src));
+  int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
+                                                    slot_bytes(k, n_chunks));
+  unsigned* rescue_cnt = scal_u + 2;
+  if (phases & (ALS_PHASE_PREP | ALS_PHASE_RSCALE | ALS_PHASE_LAUNCH1))
+    ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));
   const int cn = cn_for_k(k);
   const int kp = als_k_pad(k);
   const int zero_row = (int)n_src;
-  if (phases & 4) {  // Y_src prep: max |Y_src|, split table (explicit) / YtY table (W1 implicit)
+  if (phases & ALS_PHASE_PREP) {  // Y_src prep: max |Y_src|, split table (explicit) / YtY table (W1 implicit)
     ALS_HIP(hipMemsetAsync(scal_u, 0, sizeof(unsigned), st));
     if (implicit && cn == 8) {
       yty_ctab_kernel<<<1, 64, 0, st>>>(yty_packed, ytyC);
@@ -2490,7 +2692,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       ALS_LAUNCH_CHECK();
     }
   }
-  if (phases & 8) {  // rating scale of this block: max |rating|
+  if (phases & ALS_PHASE_RSCALE) {  // rating scale of this block: max |rating|
     ALS_HIP(hipMemsetAsync(scal_u + 1, 0, sizeof(unsigned), st));
     if (n_light + n_heavy > 0) {
       ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
@@ -2499,9 +2701,10 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       ALS_LAUNCH_CHECK();
     }
   }
-  const unsigned g1 = (phases & 1) ? (unsigned)(n_chunks + n_light_primal) : 0u;
-  const unsigned gd = (phases & 1) ? (unsigned)(n_light - n_light_primal) : 0u;
-  const unsigned g2 = (phases & 2) ? (unsigned)n_heavy : 0u;
+  const unsigned g1 = (phases & ALS_PHASE_LAUNCH1) ? (unsigned)(n_chunks + n_light_primal) : 0u;
+  const unsigned gd = (phases & ALS_PHASE_DUAL) ? (unsigned)(n_light - n_light_primal) : 0u;
+  const unsigned g2 = (phases & ALS_PHASE_LAUNCH2) ? (unsigned)n_heavy : 0u;
+  const bool rescue = (phases & ALS_PHASE_RESCUE) && !implicit && n_rows > 0;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
     if (g1)                                                                                       \
@@ -2509,23 +2712,31 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                     chunk_begin, chunk_end, n_chunks,             \
                                                     n_light_primal, Y_src, X_dst, ld, k, reg,     \
                                                     alpha, yty_packed, slots, status_dev, scal,   \
-                                                    Ysp, kp, zero_row);                           \
+                                                    Ysp, kp, zero_row, rescue_cnt, rescue_list);  \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd && CN == 4 && !IMP) {                                                                  \
       gram_solve_dual_kernel<64><<<gd, 64, 0, st>>>(row_ptr, col, val,                            \
                                                     light_rows + n_light_primal, X_dst, ld, reg,  \
-                                                    status_dev, scal, Ysp, zero_row);             \
+                                                    status_dev, scal, Ysp, zero_row, rescue_cnt,  \
+                                                    rescue_list);                                 \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
     if (g2) {                                                                                     \
-      heavy_sum_f64_kernel<Cfg<CN>::SLOT>                                                         \
+      heavy_sum_f64_kernel<Cfg<CN>::SLOT, IMP>                                                    \
           <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots);       \
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
                                                       slots, X_dst, ld, k, reg, yty_packed,       \
-                                                      status_dev);                                \
+                                                      status_dev, scal, rescue_cnt, rescue_list); \
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
+    if (rescue) {                                                                                 \
+      rescue_kernel<CN><<<kRescueGrid, 64, 0, st>>>(row_ptr, col, val, Y_src, X_dst, ld, k, reg,  \
+                                                    status_dev, rescue_cnt, rescue_list,          \
+                                                    kRescueChunk);                                \
+      ALS_LAUNCH_CHECK();                                                                         \
+      ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));                               \
+    }                                                                                             \
   } while (0)
 #define ALS_SOLVE_W1_LAUNCH(IMP)                                                                  \
   do {                                                                                            \
@@ -2534,12 +2745,14 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       gram_solve_w1_kernel<IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,    \
                                                    chunk_end, n_chunks, n_light_primal, Y_src,    \
                                                    X_dst, ld, k, reg, alpha, ytyC, slots_f,       \
-                                                   status_dev, scal, Ysp, kp, zero_row);          \
+                                                   status_dev, scal, Ysp, kp, zero_row,           \
+                                                   rescue_cnt, rescue_list);                      \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd) {                                                                                     \
       gram_solve_dual_kernel<128><<<gd, 64, 0, st>>>(row_ptr, col, val,                           \
                                                      light_rows + n_light_primal, X_dst, ld, reg, \
-                                                     status_dev, scal, Ysp, zero_row);            \
+                                                     status_dev, scal, Ysp, zero_row, rescue_cnt, \
+                                                     rescue_list);                                \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
     if (g2) {                                                                                     \
@@ -2547,9 +2760,17 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
           heavy_slot_begin, slots_f, yty_packed);                                                 \
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_w1_kernel<IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,      \
-                                                     slots_f, X_dst, ld, k, reg, status_dev);     \
+                                                     slots_f, X_dst, ld, k, reg, status_dev,      \
+                                                     scal, rescue_cnt, rescue_list);              \
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
+    if (rescue) {                                                                                 \
+      rescue_kernel<8><<<kRescueGrid, 64, 0, st>>>(row_ptr, col, val, Y_src, X_dst, ld, k, reg,   \
+                                                   status_dev, rescue_cnt, rescue_list,           \
+                                                   kRescueChunk);                                 \
+      ALS_LAUNCH_CHECK();                                                                         \
+      ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));                               \
+    }                                                                                             \
   } while (0)
   if (implicit) {
     if (cn == 1) ALS_SOLVE_LAUNCH(1, true);

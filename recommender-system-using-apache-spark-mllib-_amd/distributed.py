@@ -56,6 +56,7 @@ class HipKernels:
         self.ws = E.Workspace(self.device)
         self.chunk = chunk or E.DEFAULT_CHUNK
         self.max_chunks = 0  # heavy-row chunks of the largest block: one workspace layout
+        self.max_rows = 0    # rows of the largest block (rescue list)
 
     def index_build(self, ids: torch.Tensor, id_space: int):
         idx = self.E.build_index(ids.to(self.device, torch.int32).contiguous(), id_space, self.ws)
@@ -70,6 +71,7 @@ class HipKernels:
         blk = self.E.build_block(rows.contiguous(), ri, cols.contiguous(), ci,
                                  vals.contiguous(), self.ws, self.chunk)
         self.max_chunks = max(self.max_chunks, blk.n_chunks)
+        self.max_rows = max(self.max_rows, blk.n_light + blk.n_heavy)
         return blk
 
     def yty(self, Y: torch.Tensor, n: int, rank: int) -> torch.Tensor:
@@ -78,8 +80,10 @@ class HipKernels:
     def solve_half(self, block, Y, X, rank, reg, implicit, alpha, yty, status, first=True):
         """first=False: Y was prepared (scale, split table) by the previous call of this
         half-sweep; only this block's rating scale and launches run."""
-        self.E.solve_half(block, Y, X, rank, reg, implicit, alpha, yty, status, self.ws,
-                          phases=15 if first else 11, ws_chunks=self.max_chunks)
+        E = self.E
+        E.solve_half(block, Y, X, rank, reg, implicit, alpha, yty, status, self.ws,
+                     phases=E.PHASE_ALL if first else E.PHASE_ALL & ~E.PHASE_PREP,
+                     ws_chunks=self.max_chunks, ws_rows=self.max_rows)
 
     def predict(self, u_keys, i_keys, umap, imap, U, V, rank) -> torch.Tensor:
         E = self.E
@@ -271,13 +275,20 @@ class ShardedALS:
     def _auto_chunks(self, u_space: int, i_space: int) -> int:
         """4 row chunks when a rank's share of the larger id space reaches 1M rows
         (the all-gather then moves >= 256 MB per rank at rank 64), else 1; and at
-        least enough chunks that one chunk's all-gather (all ranks, rank <= 128
-        factors, 512 B per row) stays within MAX_COLLECTIVE_BYTES."""
+        least enough chunks that one chunk's all-gather stays within
+        MAX_COLLECTIVE_BYTES: a chunk holds at most ceil(PAD_CAP n / (W C)) rows of each
+        rank (the cap _layout applies), so the all-gather of one chunk moves at most
+        W x that x 512 B (rank <= 128 factors) — counted exactly, so the guard in
+        _solve_and_gather never stops a configuration more chunks would handle."""
         big = max(u_space, i_space)
-        need = math.ceil(PAD_CAP * big * 512 / MAX_COLLECTIVE_BYTES)
-        if self.world == 1:
-            return max(1, need)
-        return max(4 if big // self.world >= (1 << 20) else 1, need)
+        W = self.world
+        c = max(1, 4 if (W > 1 and big // W >= (1 << 20)) else 1)
+        # (a chunk of one row per rank is the floor: below it the guard decides, with
+        # the real row size)
+        while (math.ceil(PAD_CAP * big / (W * c)) > 1 and
+               W * math.ceil(PAD_CAP * big / (W * c)) * 512 > MAX_COLLECTIVE_BYTES):
+            c += 1
+        return c
 
     def _layout(self, ids: torch.Tensor, space: int, offset: int) -> SideLayout:
         dev = self.device
@@ -335,8 +346,9 @@ class ShardedALS:
         The round count is the max over ranks (every rank issues the same calls)."""
         W = self.world
         o = torch.empty(sum(rc), dtype=t.dtype, device=t.device)
+        # per-peer elements per round: one round moves at most W x per elements, so every
+        # call is within MAX_COLLECTIVE_BYTES by construction (tested with gloo)
         per = max(1, MAX_COLLECTIVE_BYTES // (t.element_size() * W))
-        _guard(min(per, max(max(sc), max(rc), 1)) * W * t.element_size(), "routing all_to_all")
         rounds_t = torch.tensor([-(-max(max(sc), max(rc), 1) // per)], dtype=torch.int64,
                                 device=dev)
         dist.all_reduce(rounds_t, op=dist.ReduceOp.MAX, group=self.group)

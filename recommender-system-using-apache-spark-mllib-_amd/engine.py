@@ -31,6 +31,21 @@ MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefr
 DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
 DUAL_MAX_RATINGS_64 = 32  # explicit, 32 < k <= 64: the same for rows this short
 
+# als_solve_half phase bits (include/als_hip.h ALS_PHASE_*)
+PHASE_LAUNCH1, PHASE_LAUNCH2, PHASE_PREP, PHASE_RSCALE, PHASE_DUAL, PHASE_RESCUE = 1, 2, 4, 8, 16, 32
+PHASE_ALL = 63
+
+
+def dual_limit(rank: int) -> int:
+    """Longest row (ratings) solved through the n x n dual system at this rank; 0 = none.
+    The dual system Y_S Y_S^T + lambda n I is full rank only while n <= rank: a longer
+    row would trade the full-rank k x k primal for a rank-deficient n x n system whose
+    smallest eigenvalues are lambda n (fp32 error growing as lambda shrinks), so the
+    limit is min(96, rank) above rank 64 and 32 (< rank) at ranks 33-64."""
+    if rank > 64:
+        return min(DUAL_MAX_RATINGS, rank)
+    return DUAL_MAX_RATINGS_64 if rank > 32 else 0
+
 
 def ld_for(rank: int) -> int:
     return (rank + 3) // 4 * 4
@@ -149,12 +164,24 @@ class RatingBlock:
     chunk_row: torch.Tensor
     chunk_begin: torch.Tensor
     chunk_end: torch.Tensor
-    n_short: int = 0  # light rows with <= DUAL_MAX_RATINGS ratings (the light list's tail)
-    n_short64: int = 0  # light rows with <= DUAL_MAX_RATINGS_64 ratings
+    # short_counts[d] = light rows with <= d ratings, d = 0..DUAL_MAX_RATINGS (host ints)
+    short_counts: tuple = ()
+    short_nnz: tuple = ()   # ratings of those rows
+
+    @property
+    def n_short(self) -> int:
+        return self.short_counts[-1] if self.short_counts else 0
 
     def n_dual(self, rank: int) -> int:
-        """Light rows solved through the n x n dual system at this rank (explicit, reg > 0)."""
-        return self.n_short if rank > 64 else (self.n_short64 if rank > 32 else 0)
+        """Light rows solved through the n x n dual system at this rank (explicit, reg > 0):
+        the tail of the longest-first light list with <= dual_limit(rank) ratings."""
+        d = dual_limit(rank)
+        return self.short_counts[d] if (d and self.short_counts) else 0
+
+    def dual_nnz(self, rank: int) -> int:
+        """Ratings of the dual-path rows at this rank."""
+        d = dual_limit(rank)
+        return self.short_nnz[d] if (d and self.short_nnz) else 0
 
 
 def build_block(row_ids: torch.Tensor, row_index: IdIndex, col_ids: torch.Tensor,
@@ -194,14 +221,17 @@ def schedule_block(n_rows, nnz, row_ptr, col, val, ws: Workspace, chunk: int = D
                                ptr(light), ptr(heavy), ptr(slot_begin), ptr(crow), ptr(cbeg),
                                ptr(cend), ptr(w), w.numel(), stream_ptr(dev)),
           "als_schedule_build")
-    n_short = n_short64 = 0
+    counts, nzs = (0,) * (DUAL_MAX_RATINGS + 1), (0,) * (DUAL_MAX_RATINGS + 1)
     if n_light > 0:  # light rows are ordered by decreasing degree: the short ones are last
         lr = light[:n_light].long()
         deg = row_ptr[lr + 1] - row_ptr[lr]
-        n_short = int((deg <= DUAL_MAX_RATINGS).sum())
-        n_short64 = int((deg <= DUAL_MAX_RATINGS_64).sum())
+        short = deg[deg <= DUAL_MAX_RATINGS]
+        h = torch.bincount(short, minlength=DUAL_MAX_RATINGS + 1).to(torch.int64)
+        w = h * torch.arange(DUAL_MAX_RATINGS + 1, device=h.device)
+        counts = tuple(int(x) for x in torch.cumsum(h, 0).tolist())
+        nzs = tuple(int(x) for x in torch.cumsum(w, 0).tolist())
     return RatingBlock(n_rows, nnz, row_ptr, col, val, chunk, n_light, n_heavy, n_chunks, light,
-                       heavy, slot_begin, crow, cbeg, cend, n_short, n_short64)
+                       heavy, slot_begin, crow, cbeg, cend, counts, nzs)
 
 
 # ---------------------------------------------------------------------------
@@ -224,24 +254,27 @@ def compute_yty(Y: torch.Tensor, n: int, rank: int, ws: Workspace) -> torch.Tens
 
 def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, reg: float,
                implicit: bool, alpha: float, yty: Optional[torch.Tensor],
-               status: torch.Tensor, ws: Workspace, phases: int = 15,
-               ws_chunks: Optional[int] = None, dual: bool = True) -> None:
+               status: torch.Tensor, ws: Workspace, phases: int = PHASE_ALL,
+               ws_chunks: Optional[int] = None, dual: bool = True,
+               ws_rows: Optional[int] = None) -> None:
     """One computeFactors pass: X[row] <- solve(A_row, b_row) for every row of `block`.
-    phases (bits, see als_hip.h): 4 = Y prep (max |Y|, split table), 8 = rating scale,
-    1 = launch 1, 2 = launch 2; 15 = all in order.  ws_chunks: size the workspace for
-    this many heavy-row chunks (>= block.n_chunks; blocks sharing one Y prep).
-    dual: explicit, reg > 0 — rows with <= DUAL_MAX_RATINGS ratings (64 < rank <= 128)
-    or <= DUAL_MAX_RATINGS_64 (32 < rank <= 64) are solved through the equivalent
-    n x n dual system (als_hip.h n_light_primal); False keeps every row on the k x k
-    normal equations."""
+    phases (PHASE_* bits, als_hip.h ALS_PHASE_*): PREP (max |Y|, split table), RSCALE
+    (rating scale), LAUNCH1 (chunk partials + primal light rows), DUAL (dual-path light
+    rows), LAUNCH2 (heavy rows), RESCUE (rows outside the split window); PHASE_ALL = all
+    in order.  ws_chunks / ws_rows: size the workspace for this many heavy-row chunks /
+    rows (blocks sharing one Y prep).
+    dual: explicit, reg > 0 — rows with <= dual_limit(rank) ratings are solved through
+    the equivalent n x n dual system (als_hip.h n_light_primal); False keeps every row
+    on the k x k normal equations."""
     L = _lib.lib()
     use_dual = dual and not implicit and reg > 0
     n_primal = block.n_light - block.n_dual(rank) if use_dual else block.n_light
-    w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0]),
-               keep_scale=True)
+    n_rows = max(block.n_light + block.n_heavy, ws_rows or 0)
+    w = ws.get(L.als_solve_workspace_bytes(rank, max(block.n_chunks, ws_chunks or 0), Y.shape[0],
+                                           n_rows), keep_scale=True)
     key = (w.data_ptr(), w.numel())
-    if (phases & 8) and ws.shared_rating_scale and ws.rating_scale_key == key:
-        phases &= ~8  # the rating scale word of this rating set is already in place
+    if (phases & PHASE_RSCALE) and ws.shared_rating_scale and ws.rating_scale_key == key:
+        phases &= ~PHASE_RSCALE  # the rating scale word of this rating set is already in place
         if phases == 0:
             return
     check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
@@ -253,7 +286,7 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
                            int(bool(implicit)),
                            float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(), int(phases),
                            stream_ptr(X.device)), "als_solve_half")
-    if (phases & 8) and ws.shared_rating_scale:
+    if (phases & PHASE_RSCALE) and ws.shared_rating_scale:
         ws.rating_scale_key = key
 
 

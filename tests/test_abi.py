@@ -52,10 +52,12 @@ def test_workspace_sizes_are_monotone_and_host_only():
     L = _lib.lib()
     assert L.als_csr_workspace_bytes(1000, 10) < L.als_csr_workspace_bytes(10 ** 7, 10 ** 5)
     assert L.als_index_workspace_bytes(10, 100) < L.als_index_workspace_bytes(10, 10 ** 6)
-    assert L.als_solve_workspace_bytes(64, 0, 1000) < L.als_solve_workspace_bytes(64, 100, 1000)
-    assert L.als_solve_workspace_bytes(10, 100, 1000) < L.als_solve_workspace_bytes(64, 100, 1000)
-    assert L.als_solve_workspace_bytes(64, 100, 1000) < L.als_solve_workspace_bytes(128, 100, 1000)
-    assert L.als_solve_workspace_bytes(64, 100, 10) < L.als_solve_workspace_bytes(64, 100, 10 ** 6)
+    ws = L.als_solve_workspace_bytes
+    assert ws(64, 0, 1000, 10) < ws(64, 100, 1000, 10)
+    assert ws(10, 100, 1000, 10) < ws(64, 100, 1000, 10)
+    assert ws(64, 100, 1000, 10) < ws(128, 100, 1000, 10)
+    assert ws(64, 100, 10, 10) < ws(64, 100, 10 ** 6, 10)
+    assert ws(64, 100, 1000, 10) + 4 * 10 ** 6 <= ws(64, 100, 1000, 10 ** 6 + 10)  # rescue list
     assert L.als_yty_workspace_bytes(10 ** 6, 64) < L.als_yty_workspace_bytes(10 ** 6, 128)
     assert L.als_yty_workspace_bytes(10 ** 6, 64) > 0
     assert L.als_rmse_workspace_bytes(10 ** 6) > L.als_rmse_workspace_bytes(10)
@@ -77,7 +79,9 @@ def _solve_args(**over):
 @pytest.mark.parametrize("over,code", [
     (dict(k=0), -4), (dict(k=129, ld=132), -4), (dict(ld=62), -1), (dict(ld=32), -1),
     (dict(n_light=-1), -1), (dict(Y=0), -1), (dict(implicit=1), -1), (dict(reg=-1.0), -1),
-    (dict(Y=18), -1), (dict(phases=0), -1), (dict(phases=16), -1), (dict(n_src=-1), -1), (dict(ws=8), -1), (dict(val=20), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2),
+    (dict(Y=18), -1), (dict(phases=0), -1), (dict(phases=64), -1), (dict(n_src=-1), -1),
+    (dict(ws=8), -1), (dict(val=20), -1), (dict(n_chunks=1 << 20, ws_bytes=16), -2),
+    (dict(n_light=1 << 28, n_light_primal=1 << 28, ws_bytes=1 << 20), -2),  # rescue list
     (dict(n_light_primal=2), -1), (dict(n_light_primal=-1), -1),
     (dict(n_light_primal=0, k=32, ld=32), -1),           # dual path needs k > 32
     (dict(n_light_primal=0, k=128, ld=128, reg=0.0), -1),  # ... and regParam > 0
@@ -87,6 +91,24 @@ def test_solve_half_argument_errors(over, code):
     rc = L.als_solve_half(*_solve_args(**over))
     assert rc == code
     assert L.als_last_error()  # a message is set
+
+
+def test_phase_bits_match_the_header():
+    from als_mi355x import engine as E
+    src = open(HEADER).read()
+    got = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define ALS_PHASE_(\w+) (\d+)", src)}
+    assert got == {"LAUNCH1": E.PHASE_LAUNCH1, "LAUNCH2": E.PHASE_LAUNCH2, "PREP": E.PHASE_PREP,
+                   "RSCALE": E.PHASE_RSCALE, "DUAL": E.PHASE_DUAL, "RESCUE": E.PHASE_RESCUE,
+                   "ALL": E.PHASE_ALL}
+    assert E.PHASE_ALL == sum(v for k, v in got.items() if k != "ALL")
+
+
+def test_dual_limit_keeps_the_dual_system_full_rank():
+    from als_mi355x import engine as E
+    for k in range(1, 129):
+        d = E.dual_limit(k)
+        assert d <= k and d <= E.DUAL_MAX_RATINGS
+        assert d == (min(96, k) if k > 64 else (32 if k > 32 else 0))
 
 
 def test_topk_and_predict_argument_errors():

@@ -20,7 +20,7 @@ def bench():
 
 
 def _block(n_light, n_chunks, n_short, n_short64):
-    blk = SimpleNamespace(n_light=n_light, n_chunks=n_chunks, n_short=n_short, n_short64=n_short64)
+    blk = SimpleNamespace(n_light=n_light, n_chunks=n_chunks)
     blk.n_dual = lambda rank: n_short if rank > 64 else (n_short64 if rank > 32 else 0)
     return blk
 
@@ -33,6 +33,22 @@ def test_launch1_parts_name_the_dual_kernel(bench):
         ("gram_solve_kernel<4,false>", 64 * (10 + 800)), ("gram_solve_dual_kernel<64>", 64 * 200)]
     assert bench._launch1_parts(b, 128, True) == [("gram_solve_w1_kernel<true>", 64 * 1010)]
     assert bench._launch1_parts(b, 16, False) == [("gram_solve_kernel<1,false>", 64 * 1010)]
+    assert bench._launch1_parts(b, 128, False, reg=0.0) == [("gram_solve_w1_kernel<false>", 64 * 1010)]
+
+
+def test_bench_refuses_a_redirected_library(tmp_path):
+    import subprocess
+    import sys
+    env = dict(os.environ, ALS_HIP_LIB=str(tmp_path / "libdev.so"))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-big"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "ALS_HIP_LIB" in p.stderr
+
+
+def test_library_record_names_the_in_tree_build(bench):
+    rec = bench.library_record()
+    assert rec["path"].endswith("libals_hip.so") and not rec["path"].startswith("..")
+    assert len(rec["sha256"]) == 64
 
 
 def test_phase_counters_combine_by_grid(bench, monkeypatch):

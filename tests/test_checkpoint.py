@@ -105,6 +105,30 @@ def test_auto_resume_requires_the_same_initialisation(tmp_path):
     assert C.resume_point(d, True, e, 3, 0.1, False, 1.0, 10, C.init_key(8, None))[0] == 2
 
 
+def test_format1_checkpoint_auto_skips_with_warning_and_is_cleaned(tmp_path):
+    """A round-2 (format-1) checkpoint has its files next to the JSON and no
+    initialisation record: "auto" skips it with a warning, resume=True continues from
+    it, and the first format-2 save removes the old top-level files."""
+    import json
+    e = _eng()
+    d = tmp_path / "ck"
+    d.mkdir()
+    for name, arr in ((C.IDS, e.ids), (C.FACTORS, e.U), (C.IIDS, np.arange(5, dtype=np.int32)),
+                      (C.IFACTORS, e.V)):
+        np.save(d / name, arr, allow_pickle=False)
+    (d / C.STATE).write_text(json.dumps({"format": 1, "iteration": 2, "rank": 3, "regParam": 0.1,
+                                         "implicitPrefs": False, "alpha": 1.0, "data": e.data}))
+    with pytest.warns(UserWarning, match="initialisation record"):
+        assert C.resume_point(str(d), "auto", e, 3, 0.1, False, 1.0, 10,
+                              C.init_key(1, None)) == (0, None, None)
+    start, U, _ = C.resume_point(str(d), True, e, 3, 0.1, False, 1.0, 10, C.init_key(1, None))
+    assert start == 2
+    np.testing.assert_array_equal(U, e.U)
+    C.maybe_save(str(d), 1, 3, e, 3, 0.1, False, 1.0, init=C.init_key(1, None))
+    assert sorted(p.name for p in d.iterdir() if p.suffix == ".npy") == []
+    assert C.load(str(d)).iteration == 3
+
+
 def test_resume_point_rules(tmp_path):
     e = _eng()
     d = str(tmp_path / "ck")

@@ -1,4 +1,4 @@
-"""Multi-process (world_size 2, gloo, CPU) test of the sharded ALS coordination
+"""Multi-process (world_size 2 and 8, gloo, CPU) test of the sharded ALS coordination
 (als_mi355x.distributed.ShardedALS): id-space agreement, nnz-balanced row
 ranges, the one-time all_to_all rating routing, padded factor layout, per
 half-sweep all_gather and the implicit YtY all_reduce.
@@ -105,7 +105,7 @@ def _worker(rank, world, port, implicit, chunks, out_dir):
     uid, Uf = K.user_factors()
     iid, Vf = K.item_factors()
     if rank == 0:
-        np.savez(os.path.join(out_dir, f"dist_{int(implicit)}_{chunks}.npz"), uid=uid.numpy(),
+        np.savez(os.path.join(out_dir, f"dist_{int(implicit)}_{chunks}_{world}.npz"), uid=uid.numpy(),
                  U=Uf.numpy(), iid=iid.numpy(), V=Vf.numpy(), nnz=K.nnz,
                  u_starts=K.users.starts.numpy(), i_starts=K.items.starts.numpy(),
                  local=[K.user_rows, K.item_rows])
@@ -184,13 +184,15 @@ def test_sharded_serving_matches_oracle(tmp_path, world):
     np.testing.assert_array_equal(d["sids"][0], uids[ref_u[0]])
 
 
-@pytest.mark.parametrize("implicit,chunks", [(False, None), (True, None), (False, 3), (True, 3)])
-def test_sharded_als_matches_single_process(tmp_path, implicit, chunks):
-    """chunks=3: the [C, world, rows] layout with async per-chunk all-gathers."""
-    world = 2
+@pytest.mark.parametrize("implicit,chunks,world", [(False, None, 2), (True, None, 2), (False, 3, 2),
+                                                  (True, 3, 2), (False, 2, 8), (True, None, 8)])
+def test_sharded_als_matches_single_process(tmp_path, implicit, chunks, world):
+    """chunks=3: the [C, world, rows] layout with async per-chunk all-gathers.  world 8:
+    the target world size of BASELINE configs[3] (8 x MI355X), every rank a range of
+    ~15 users and ~11 items, the full 3-iteration fit against the single-process oracle."""
     mp.spawn(_worker, args=(world, _free_port(), implicit, chunks, str(tmp_path)), nprocs=world,
              join=True)
-    d = np.load(tmp_path / f"dist_{int(implicit)}_{chunks}.npz")
+    d = np.load(tmp_path / f"dist_{int(implicit)}_{chunks}_{world}.npz")
     from oracle import als_oracle as O
     u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
     if implicit:
@@ -279,6 +281,21 @@ def _resume_worker(rank, world, port, out_dir, mode):
         K.fit(5, 4, 0.1, seed=7, checkpoint_dir=ck_r, checkpoint_interval=0, resume="auto")
     elif mode == "auto99":  # other seed: a different fit, "auto" starts fresh
         K.fit(5, 4, 0.1, seed=99, checkpoint_dir=ck_r, checkpoint_interval=0, resume="auto")
+    elif mode == "broken":  # the generation directory named by als_state.json is gone
+        import json
+        import shutil
+        if rank == 0:
+            gen = json.load(open(os.path.join(ck, "als_state.json")))["generation"]
+            shutil.rmtree(os.path.join(ck, gen))
+        err = ""
+        try:
+            K.fit(5, 4, 0.1, seed=7, checkpoint_dir=ck_r, checkpoint_interval=0, resume="auto")
+        except RuntimeError as e:
+            err = str(e)
+        np.save(os.path.join(out_dir, f"broken_{rank}.npy"),
+                np.array([float("unreadable" in err)]))
+        dist.destroy_process_group()
+        return
     else:  # "at": nothing left to run, U and V come from the checkpoint
         K.fit(5, 2, 0.1, seed=99, checkpoint_dir=ck_r, checkpoint_interval=0, resume=True)
     _, Uf = K.user_factors()
@@ -311,6 +328,11 @@ def test_checkpoint_resume_across_world_sizes(tmp_path):
     at = np.load(tmp_path / "at_w2.npz")
     np.testing.assert_array_equal(at["U"], st.U)
     np.testing.assert_array_equal(at["V"], st.V)
+    # a checkpoint whose generation directory is missing: process 0 fails to read it
+    # and the failure is broadcast, so every rank raises (none waits in a collective)
+    mp.spawn(_resume_worker, args=(2, _free_port(), str(tmp_path), "broken"), nprocs=2, join=True)
+    for w in range(2):
+        assert np.load(tmp_path / f"broken_{w}.npy")[0] == 1.0
 
 
 def _surface_worker(rank, world, port, out_dir):
@@ -453,6 +475,26 @@ def test_padding_bounded_with_popularity_ordered_ids(tmp_path, world):
     pu, pi, diff = np.load(tmp_path / f"pad_{world}.npy")
     assert pu <= 1.25 + 1e-9 and pi <= 1.25 + 1e-9, (pu, pi)
     assert diff <= 1e-4
+
+
+def test_auto_chunks_keep_every_chunk_gather_within_the_cap():
+    """_auto_chunks counts a chunk's all-gather exactly (W x the per-chunk row cap x
+    512 B), for world sizes that are not powers of two too, and adds no chunk beyond
+    what the cap needs."""
+    import math
+    from types import SimpleNamespace
+    import _pkgload
+    _pkgload.load()
+    from als_mi355x import distributed as Dm
+    for W in (1, 2, 3, 5, 6, 7, 8):
+        for big in (1000, 162_541, 1_000_000, 10_000_000, 10_000_019, 123_456_789):
+            c = Dm.ShardedALS._auto_chunks(SimpleNamespace(world=W), big, 7)
+            rows = math.ceil(Dm.PAD_CAP * big / (W * c))
+            assert W * rows * 512 <= Dm.MAX_COLLECTIVE_BYTES, (W, big, c)
+            floor = 4 if (W > 1 and big // W >= (1 << 20)) else 1
+            if c > floor:  # one chunk fewer would break the cap
+                assert W * math.ceil(Dm.PAD_CAP * big / (W * (c - 1))) * 512 > \
+                    Dm.MAX_COLLECTIVE_BYTES
 
 
 def _guard_worker(rank, world, port, out_dir):

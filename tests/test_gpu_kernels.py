@@ -258,20 +258,25 @@ def _degree_data(degrees, n_items, seed):
 DUAL_DEGREES = [1, 2, 7, 15, 16, 17, 31, 32, 33, 40, 48, 63, 64, 65, 66, 90, 96, 97, 128, 129]
 
 
-@pytest.mark.parametrize("rank", [33, 40, 64, 65, 96, 100, 128])
-def test_dual_short_rows_match_primal_and_oracle(rank):
-    """Explicit rows with <= 96 ratings at rank 65-128 go through the n x n dual
-    system (NB = 2 for n <= 32, 4 for n <= 64, 6 for n <= 96), rows with <= 32 ratings
-    at rank 33-64 too (NB = 2, split table of 64 words per row); the rest through the
-    k x k primal.  Both forms vs the fp64 oracle of Spark's k x k normal equations, per
-    row, with the degrees around every class boundary (1, 16/17, 32/33, 64/65, 96/97)."""
-    degrees = DUAL_DEGREES * 15
+@pytest.mark.parametrize("rank,reg", [(33, 0.1), (40, 0.1), (64, 0.1), (65, 0.1), (96, 0.1),
+                                      (100, 0.1), (128, 0.1), (65, 1e-3), (80, 1e-3), (95, 1e-3),
+                                      (80, 1e-4), (128, 1e-3)])
+def test_dual_short_rows_match_primal_and_oracle(rank, reg):
+    """Explicit rows with <= min(96, rank) ratings at rank 65-128 go through the n x n
+    dual system (NB = 2 for n <= 32, 4 for n <= 64, 6 for n <= 96), rows with <= 32
+    ratings at rank 33-64 too (NB = 2, split table of 64 words per row); the rest
+    through the k x k primal.  The limit min(96, rank) keeps the dual system full rank
+    (n <= k): at rank 65-95 the rows with rank < n <= 96 stay primal, which the small
+    regParams (1e-3, 1e-4) would otherwise expose.  Both forms vs the fp64 oracle of
+    Spark's k x k normal equations, per row, with the degrees around every class
+    boundary (1, 16/17, 32/33, 64/65, 96/97) and at the rank limit."""
+    degrees = (DUAL_DEGREES + [rank - 1, rank, rank + 1]) * 15
     u, i, r = _degree_data(degrees, 400, seed=rank)
     core = _core(u, i, r, chunk=256)
     ub = core.user_block
     assert ub.n_short == sum(d <= E.DUAL_MAX_RATINGS for d in degrees)
-    assert ub.n_short64 == sum(d <= E.DUAL_MAX_RATINGS_64 for d in degrees)
-    assert ub.n_dual(rank) == (ub.n_short if rank > 64 else ub.n_short64)
+    assert ub.n_dual(rank) == sum(d <= E.dual_limit(rank) for d in degrees)
+    assert E.dual_limit(rank) == (min(96, rank) if rank > 64 else 32)
     core.init_factors(rank, seed=3)
     g = torch.Generator(device=DEV)
     g.manual_seed(rank)
@@ -280,13 +285,13 @@ def test_dual_short_rows_match_primal_and_oracle(rank):
     core.V[:, :rank] = V0
     V0 = V0.cpu().numpy()
     U_ref = O.half_sweep(ub.row_ptr.cpu().numpy(), ub.col.cpu().numpy(), ub.val.cpu().numpy(),
-                         V0, 0.1)
+                         V0, reg)
     deg = np.diff(ub.row_ptr.cpu().numpy())
     out = {}
     for dual in (True, False):
         core.U.fill_(7.0)  # every written entry must be overwritten (pad columns with 0)
         core.status.zero_()
-        E.solve_half(ub, core.V, core.U, rank, 0.1, False, 1.0, None, core.status, core.ws,
+        E.solve_half(ub, core.V, core.U, rank, reg, False, 1.0, None, core.status, core.ws,
                      dual=dual)
         torch.cuda.synchronize()
         core.check_status()
@@ -296,7 +301,104 @@ def test_dual_short_rows_match_primal_and_oracle(rank):
         out[dual] = {f"deg<={b}": float(e[(deg <= b) & (deg > a)].max())
                      for a, b in ((0, 16), (16, 32), (32, 64), (64, 10 ** 9))}
         assert e.max() <= 1e-4, (dual, out[dual])
-    report(f"dual_vs_primal[rank={rank}]", out)
+    report(f"dual_vs_primal[rank={rank},reg={reg:g}]", out)
+
+
+def _exact_rel_errs(x, ref):
+    """Per-row ||x - ref|| / ||ref|| with no floor (rows of any magnitude)."""
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    nr = np.linalg.norm(ref, axis=1)
+    e = np.linalg.norm(x - ref, axis=1) / np.where(nr > 0, nr, 1.0)
+    e[nr == 0] = np.linalg.norm(x[nr == 0], axis=1)
+    return e
+
+
+@pytest.mark.parametrize("spread", [1e7, 1e9])
+@pytest.mark.parametrize("rank", [16, 48, 64, 100, 128])
+def test_split_window_row_norm_spread(spread, rank):
+    """Split window guard: the explicit Gram uses one power-of-two scale
+    per launch, so factor rows far below the launch maximum would reach subnormal f16
+    lo halves.  A block of users whose factors are 1/spread of the rest rates its own
+    items (light rows, dual-path short rows and one heavy, chunked item): those items'
+    systems see only tiny factor rows and must still match the fp64 oracle to 1e-4
+    per row — relative to their own norm — via the rescue launch."""
+    u1, i1, r1 = planted(500, 300, density=0.05, heavy_items=(3,), seed=31)
+    u2, i2, r2 = planted(400, 120, density=0.08, heavy_items=(5,), seed=32)  # tiny users' items
+    u = np.concatenate([u1, u2 + 500]).astype(np.int32)
+    i = np.concatenate([i1, i2 + 300]).astype(np.int32)
+    r = np.concatenate([r1, r2]).astype(np.float32)
+    core = _core(u, i, r, chunk=128)
+    core.init_factors(rank, seed=3)
+    core.U[500:] /= spread
+    U0 = core.U[:, :rank].cpu().numpy()
+    core.half_sweep_items(0.1, False, 1.0)
+    torch.cuda.synchronize()
+    core.check_status()
+    ib = core.item_block
+    V_ref = O.half_sweep(ib.row_ptr.cpu().numpy(), ib.col.cpu().numpy(), ib.val.cpu().numpy(),
+                         U0, 0.1)
+    e = _exact_rel_errs(core.V[:, :rank].cpu().numpy(), V_ref)
+    tiny = np.arange(300, 420)  # dense rows = ids (all present)
+    report(f"split_window_norm_spread[{spread:g},rank={rank}]",
+           {"tiny_rows": float(e[tiny].max()), "other_rows": float(np.delete(e, tiny).max())})
+    assert e.max() <= 1e-4, (e[tiny].max(), np.delete(e, tiny).max())
+    # and the reverse direction: the tiny items' factors feed a user half-sweep
+    core.V[:, :rank] = torch.as_tensor(V_ref).to(DEV)
+    core.half_sweep_users(0.1, False, 1.0)
+    ub = core.user_block
+    U_ref = O.half_sweep(ub.row_ptr.cpu().numpy(), ub.col.cpu().numpy(), ub.val.cpu().numpy(),
+                         V_ref, 0.1)
+    eu = _exact_rel_errs(core.U[:, :rank].cpu().numpy(), U_ref)
+    assert eu.max() <= 1e-4
+
+
+@pytest.mark.parametrize("rank", [8, 64, 128])
+def test_split_window_rating_spread(rank):
+    """Ratings spanning nine decades: users whose ratings are all ~1e-9 of the block's
+    largest rating (the rhs split's lo halves would be subnormal) are re-solved with
+    their own scale; every row matches the oracle to 1e-4 of its own norm."""
+    u, i, r = planted(600, 300, density=0.06, heavy_users=(2,), seed=41)
+    rng = np.random.default_rng(5)
+    scale = np.where(u % 3 == 0, 1e-9, np.where(u % 3 == 1, 1.0, 1e3)).astype(np.float64)
+    r = (r * scale * rng.uniform(0.5, 1.5, r.size)).astype(np.float32)
+    core = _core(u, i, r, chunk=128)
+    core.init_factors(rank, seed=4)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(9)
+    V0 = torch.randn((core.n_items, rank), generator=g, device=DEV)
+    core.V[:, :rank] = V0
+    core.half_sweep_users(0.1, False, 1.0)
+    torch.cuda.synchronize()
+    core.check_status()
+    ub = core.user_block
+    U_ref = O.half_sweep(ub.row_ptr.cpu().numpy(), ub.col.cpu().numpy(), ub.val.cpu().numpy(),
+                         V0.cpu().numpy(), 0.1)
+    e = _exact_rel_errs(core.U[:, :rank].cpu().numpy(), U_ref)
+    report(f"split_window_rating_spread[rank={rank}]", float(e.max()))
+    assert e.max() <= 1e-4
+
+
+@pytest.mark.parametrize("rank", [16, 64, 128])
+def test_implicit_counts_spanning_six_decades(rank):
+    """Implicit feedback with counts 1..1e6 (alpha 1): the confidence weights span six
+    decades.  No rescue is needed here (A holds YtY, b is fp32), and every row must
+    match the oracle to 1e-4."""
+    u, i, _ = planted(500, 300, density=0.06, heavy_items=(4,), seed=43)
+    rng = np.random.default_rng(6)
+    r = np.round(10.0 ** rng.uniform(0, 6, u.size)).astype(np.float32)
+    core = _core(u, i, r, chunk=128)
+    core.init_factors(rank, seed=5)
+    U0 = core.U[:, :rank].cpu().numpy()
+    core.half_sweep_items(0.1, True, 1.0)
+    torch.cuda.synchronize()
+    core.check_status()
+    ib = core.item_block
+    V_ref = O.half_sweep(ib.row_ptr.cpu().numpy(), ib.col.cpu().numpy(), ib.val.cpu().numpy(),
+                         U0, 0.1, True, 1.0)
+    e = _exact_rel_errs(core.V[:, :rank].cpu().numpy(), V_ref)
+    report(f"implicit_counts_1_1e6[rank={rank}]", float(e.max()))
+    assert e.max() <= 1e-4
 
 
 def test_failed_pivot_raises_with_row():

@@ -1299,6 +1299,17 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 // 8.1 ms/iter measured).
 template <int NB>
 constexpr bool kW1SplitSchur = NB == 8;
+// Split-f16 Schur / Pm products in the explicit light-row solves (A/B under test):
+// the k <= 64 W1<4> solve, the rank-65-128 W1 light rows and the n x n dual systems.
+#ifndef ALS_K64_SPLIT
+#define ALS_K64_SPLIT 0
+#endif
+#ifndef ALS_W1E_SPLIT
+#define ALS_W1E_SPLIT 0
+#endif
+#ifndef ALS_DUAL_SPLIT
+#define ALS_DUAL_SPLIT 0
+#endif
 
 // fp32 form: acc += X^T Y (the MFMA's k index is permuted to 4q + s4).
 __device__ __forceinline__ floatx4 tile_xty(const floatx4& X, const floatx4& Y, floatx4 acc) {
@@ -1784,7 +1795,7 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     // rank 33-64 explicit: the W1 block elimination on 4 x 4 tiles (swept diagonal
     // inverses + fp32 MFMA), in the Gram's scale
     static_assert(W1LdsT<4>::SIZE <= PanelLds<4>::SIZE, "W1<4> LDS");
-    w1_finish_and_solve<false, 4>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
+    w1_finish_and_solve<false, 4, (bool)ALS_K64_SPLIT>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
                                   X + (int64_t)row * ld, ld, row, status);
   } else {
     finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty,
@@ -2063,7 +2074,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
+  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT || (bool)ALS_W1E_SPLIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
                                                X + (int64_t)row * ld, ld, row, status);
 }
 
@@ -2196,7 +2207,7 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   float bcol[NB], z[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) bcol[c] = rc[c] * inv;
-  const bool ok = w1_solve_x<NB, false>(acc, bcol, lds, n, z);
+  const bool ok = w1_solve_x<NB, (bool)ALS_DUAL_SPLIT>(acc, bcol, lds, n, z);
   if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
   // x = Y_S^T z: z split into f16 hi + lo after a power-of-two scale
   float zm = 0.f;

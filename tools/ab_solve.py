@@ -1,0 +1,72 @@
+"""Dev A/B timing of half-sweep variants (NOT the bench): one workload, the library
+named by ALS_HIP_LIB (a tools/ab/build_solve.sh build) or the product one.
+    ALS_HIP_LIB=tools/ab/libals_x.so python tools/ab_solve.py c1|c2|c3 [steps]
+Prints one JSON line: ms per iteration and the event time of each phase launch."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+import _pkgload  # noqa: E402
+
+_pkgload.load()
+from als_mi355x import datasets as D, engine as E  # noqa: E402
+
+
+def main():
+    wl = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    dev = torch.device("cuda", 0)
+    if wl == "c3":
+        u, i, r = D.big_config("big1b", device=dev)
+        k, imp, alpha, warm = 128, False, 1.0, 1
+        steps = min(steps, 3)
+    else:
+        u, i, r = D.synthetic_config("ml25m", device=dev)
+        k, imp, alpha, warm = (64, False, 1.0, 3) if wl == "c1" else (128, True, 40.0, 3)
+    core = E.ALSCore(u, i, r, device=dev)
+    del u, i, r
+    torch.cuda.empty_cache()
+    core.init_factors(k, seed=5)
+    reg = 0.1
+    ev = {}
+
+    def half(block, Y, X, yty, name, rec):
+        E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
+                     E.PHASE_PREP | E.PHASE_RSCALE)
+        for ph, tag in ((E.PHASE_LAUNCH1, "l1"), (E.PHASE_DUAL, "dual"),
+                        (E.PHASE_LAUNCH2 | E.PHASE_RESCUE, "l2")):
+            if rec:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+            E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, ph)
+            if rec:
+                b.record()
+                ev.setdefault(f"{name}_{tag}", []).append((a, b))
+
+    def it(rec):
+        yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
+        half(core.item_block, core.U, core.V, yty, "item", rec)
+        yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
+        half(core.user_block, core.V, core.U, yty, "user", rec)
+
+    for _ in range(warm):
+        it(False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        it(True)
+    torch.cuda.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0) / steps
+    core.check_status()
+    out = {"wl": wl, "lib": os.environ.get("ALS_HIP_LIB", "product"), "ms_per_iter": round(ms, 4)}
+    for key, lst in ev.items():
+        out[key] = round(sum(a.elapsed_time(b) for a, b in lst) / len(lst), 4)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

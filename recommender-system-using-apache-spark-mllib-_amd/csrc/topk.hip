@@ -489,9 +489,15 @@ __device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
 // stream (the first tiles re-staged: compute / LDS only).
 // Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
 // rows), 4 with LDS lists (top > 128: the lists of 64 RG rows fill the LDS).
-__host__ __device__ constexpr int tk_nw(int topr) { return topr > 0 ? 8 : 4; }
+// Quad lists with two row groups (RG = 2): 4 wavefronts of 32 query rows each, one
+// wavefront per SIMD (the lists of 32 rows take 100 VGPRs at top 100): every V tile
+// read from LDS feeds two MFMAs per k-step (as the top <= 16 kernel's two groups),
+// half the B-operand reads per score of RG = 1.
+__host__ __device__ constexpr int tk_nw(int topr, int rg = 1) {
+  return topr > 16 && rg == 2 ? 4 : (topr > 0 ? 8 : 4);
+}
 template <int NK, int RG, int TOPR, int MODE = 0>
-__global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
+__global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
                                                          const uint4* __restrict__ Vlo,
                                                          const int32_t* __restrict__ perm,
@@ -500,7 +506,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
                                                          const float* __restrict__ scal,
                                                          int32_t* __restrict__ idx_out,
                                                          float* __restrict__ score_out) {
-  constexpr int NW = tk_nw(TOPR);      // wavefronts
+  constexpr int NW = tk_nw(TOPR, RG);  // wavefronts
   constexpr int NT = 64 * NW;          // threads
   constexpr int GR = 16 * NW;          // query rows of a row group
   constexpr int KQ = 32 * NK;
@@ -584,13 +590,16 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
   // sub-list of row m (every lane: sub-list q)
   constexpr bool QUAD = TOPR > 16;
-  static_assert(!QUAD || (RG == 1 && TOPR % 4 == 0), "quad lists: one row group");
+  static_assert(!QUAD || ((RG == 1 || RG == 2) && TOPR % 4 == 0), "quad lists: 1 or 2 row groups");
   // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
   constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
+  constexpr int KG = QUAD ? RG : 1;  // quad: one sub-list per row group in every lane
   const int ncap = QUAD ? top / 4 + (q < top % 4 ? 1 : 0) : top;  // live slots of this list
-  uint64_t kv[NR];
+  uint64_t kv[KG][NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) kv[j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) kv[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
 
   // Tiles in flight in registers: DEPTH sets; after tile t is scored, tile t + 1 is
   // staged from set t % DEPTH, which then loads tile t + 1 + DEPTH.  Two sets with
@@ -721,33 +730,43 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       }
       asm volatile("" ::: "memory");  // LDS is in order within the wave
       if constexpr (QUAD) {
-        // every lane: sub-list q of row m; one candidate per row per pass
+        // every lane: sub-list q of row m of each group; one candidate per row and
+        // group per pass
         const int rho = m;
-        // this row's ballot among the four (wave-uniform) ones: masked merges, the
-        // masks opaque to the compiler (a select chain on a lane-varying index is
-        // otherwise turned into a private-memory table lookup)
-        uint64_t bb = b[0][0];
+        unsigned msk[KG];
 #pragma unroll
-        for (int t = 1; t < 4; ++t) {
-          uint64_t sel = (rho & 3) == t ? ~0ull : 0ull;
-          asm volatile("" : "+v"(sel));
-          bb = (bb & ~sel) | (b[0][t] & sel);
+        for (int g = 0; g < KG; ++g) {
+          // this row's ballot among the four (wave-uniform) ones: masked merges, the
+          // masks opaque to the compiler (a select chain on a lane-varying index is
+          // otherwise turned into a private-memory table lookup)
+          uint64_t bb = b[g][0];
+#pragma unroll
+          for (int t = 1; t < 4; ++t) {
+            uint64_t sel = (rho & 3) == t ? ~0ull : 0ull;
+            asm volatile("" : "+v"(sel));
+            bb = (bb & ~sel) | (b[g][t] & sel);
+          }
+          msk[g] = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
         }
-        unsigned msk = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
-        const float* sg = st + rho;
-        while (__ballot(msk != 0)) {
-          const bool act = msk != 0;
-          const int mm = act ? __builtin_ctz(msk) : 0;
-          msk &= msk - 1;
-          const float sc = sg[16 * mm];
+        auto pass = [&](int g) {
+          const bool act = msk[g] != 0;
+          const int mm = act ? __builtin_ctz(msk[g]) : 0;
+          msk[g] &= msk[g] - 1;
+          const float sc = st[g * 256 + rho + 16 * mm];
           const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
-          const uint64_t gmin = tk_quad_min(kv[0]);
+          const uint64_t gmin = tk_quad_min(kv[g][0]);
           // the lowest sub-list whose [0] is the row minimum takes the candidate
-          const uint64_t holders = (__ballot(kv[0] == gmin) >> rho) & 0x0001000100010001ull;
-          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv, c);
+          const uint64_t holders = (__ballot(kv[g][0] == gmin) >> rho) & 0x0001000100010001ull;
+          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv[g], c);
+        };
+#pragma unroll
+        for (int g = 0; g < KG; ++g)
+          while (__ballot(msk[g] != 0)) pass(g);
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          const uint64_t gmin = tk_quad_min(kv[g][0]);
+          if (q == 0) thr[16 * g + rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
         }
-        const uint64_t gmin = tk_quad_min(kv[0]);
-        if (q == 0) thr[rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
       } else if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
         const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
         uint64_t bb = b[0][0];
@@ -760,16 +779,22 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
           msk &= msk - 1;
           const float sc = sg[16 * mm];
           const uint64_t c = tk_key(sc, bperm[mm]);
-          if (sc == sc && c > kv[0]) tk_insert<NR>(kv, c);
+          if (sc == sc && c > kv[0][0]) tk_insert<NR>(kv[0], c);
         }
-        thr[lane] = kv[0] == kTkKeyOpen ? -__builtin_inff() : tk_key_score(kv[0]);
+        thr[lane] = kv[0][0] == kTkKeyOpen ? -__builtin_inff() : tk_key_score(kv[0][0]);
       }
       asm volatile("" ::: "memory");
       refresh();
       if (!full) {
-        const bool open_list =
-            QUAD ? (((live[0] >> m) & 1u) && kv[0] == kTkKeyOpen)
-                 : (lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) && kv[0] == kTkKeyOpen);
+        bool open_list = false;
+        if constexpr (QUAD) {
+#pragma unroll
+          for (int g = 0; g < KG; ++g)
+            open_list = open_list || (((live[g] >> m) & 1u) && kv[g][0] == kTkKeyOpen);
+        } else {
+          open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
+                      kv[0][0] == kTkKeyOpen;
+        }
         full = __ballot(open_list) == 0;
       }
       return;
@@ -887,59 +912,63 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   if constexpr (QUAD) {
     // output position of a real entry = number of real entries above it in the
     // row's four sub-lists; open slots (fewer than `top` V rows) fill the tail
-    const int64_t row = qbase + 16 * w + m;
-    const bool zero = !((live[0] >> m) & 1u);
-    int rank[NR];
-    int nreal = 0, nopen = 0;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      nreal += (kv[i] != kTkKeyOpen && kv[i] != kTkKeySentinel) ? 1 : 0;
-      nopen += (i < ncap && kv[i] == kTkKeyOpen) ? 1 : 0;
-    }
+    for (int g = 0; g < KG; ++g) {
+      const uint64_t (&kg)[NR] = kv[g];
+      const int64_t row = qbase + GR * g + 16 * w + m;
+      const bool zero = !((live[g] >> m) & 1u);
+      int rank[NR];
+      int nreal = 0, nopen = 0;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      rank[i] = 0;
-#pragma unroll
-      for (int t = i + 1; t < NR; ++t) rank[i] += kv[t] != kTkKeySentinel ? 1 : 0;
-    }
-    auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
-      constexpr int P = decltype(pc)::value;
-#pragma unroll
-      for (int t = 0; t < NR; ++t) {
-        const uint64_t o = P == 1 ? tk_partner64<16>(kv[t])
-                                  : (P == 2 ? tk_partner64<32>(kv[t])
-                                            : tk_partner64<32>(tk_partner64<16>(kv[t])));
-        if (o != kTkKeySentinel) {
-#pragma unroll
-          for (int i = 0; i < NR; ++i) rank[i] += o > kv[i] ? 1 : 0;
-        }
+      for (int i = 0; i < NR; ++i) {
+        nreal += (kg[i] != kTkKeyOpen && kg[i] != kTkKeySentinel) ? 1 : 0;
+        nopen += (i < ncap && kg[i] == kTkKeyOpen) ? 1 : 0;
       }
-    };
-    count_above(std::integral_constant<int, 1>{});
-    count_above(std::integral_constant<int, 2>{});
-    count_above(std::integral_constant<int, 3>{});
-    const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
-    const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
-    const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
-    const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
-    const int R = nreal + r1 + r2 + r3;
-    const int obase = R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
-    if (row < n_q) {
-      if (zero) {  // every score 0: the first `top` rows, ties by index
-        if (q == 0) {
-          for (int e = 0; e < top; ++e) {
-            idx_out[row * top + e] = e < n_v ? e : -1;
-            score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+#pragma unroll
+      for (int i = 0; i < NR; ++i) {
+        rank[i] = 0;
+#pragma unroll
+        for (int t = i + 1; t < NR; ++t) rank[i] += kg[t] != kTkKeySentinel ? 1 : 0;
+      }
+      auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
+        constexpr int P = decltype(pc)::value;
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+          const uint64_t o = P == 1 ? tk_partner64<16>(kg[t])
+                                    : (P == 2 ? tk_partner64<32>(kg[t])
+                                              : tk_partner64<32>(tk_partner64<16>(kg[t])));
+          if (o != kTkKeySentinel) {
+#pragma unroll
+            for (int i = 0; i < NR; ++i) rank[i] += o > kg[i] ? 1 : 0;
           }
         }
-      } else {
+      };
+      count_above(std::integral_constant<int, 1>{});
+      count_above(std::integral_constant<int, 2>{});
+      count_above(std::integral_constant<int, 3>{});
+      const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
+      const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
+      const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
+      const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
+      const int R = nreal + r1 + r2 + r3;
+      const int obase = R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
+      if (row < n_q) {
+        if (zero) {  // every score 0: the first `top` rows, ties by index
+          if (q == 0) {
+            for (int e = 0; e < top; ++e) {
+              idx_out[row * top + e] = e < n_v ? e : -1;
+              score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
+            }
+          }
+        } else {
 #pragma unroll
-        for (int i = 0; i < NR; ++i) {
-          if (i < ncap) {
-            const bool real = kv[i] != kTkKeyOpen;
-            const int64_t e = row * top + (real ? rank[i] : obase + i);
-            idx_out[e] = real ? tk_key_index(kv[i]) : -1;
-            score_out[e] = real ? tk_key_score(kv[i]) * unscale : -__builtin_inff();
+          for (int i = 0; i < NR; ++i) {
+            if (i < ncap) {
+              const bool real = kg[i] != kTkKeyOpen;
+              const int64_t e = row * top + (real ? rank[i] : obase + i);
+              idx_out[e] = real ? tk_key_index(kg[i]) : -1;
+              score_out[e] = real ? tk_key_score(kg[i]) * unscale : -__builtin_inff();
+            }
           }
         }
       }
@@ -958,9 +987,9 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
               idx_out[row * top + e] = e < n_v ? e : -1;
               score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
             } else {
-              const bool real = kv[j] != kTkKeyOpen;
-              idx_out[row * top + e] = real ? tk_key_index(kv[j]) : -1;
-              score_out[row * top + e] = real ? tk_key_score(kv[j]) * unscale : -__builtin_inff();
+              const bool real = kv[0][j] != kTkKeyOpen;
+              idx_out[row * top + e] = real ? tk_key_index(kv[0][j]) : -1;
+              score_out[row * top + e] = real ? tk_key_score(kv[0][j]) * unscale : -__builtin_inff();
             }
           }
         }
@@ -986,15 +1015,26 @@ static bool topk_quad(int top, int64_t n_v) {
   return top > kTopR && top <= kTopQ;
 }
 
+// Quad lists with two row groups per wavefront (tk_nw): A/B under test.
+#ifndef ALS_TK_QUAD_RG
+#define ALS_TK_QUAD_RG 1
+#endif
+constexpr int kTkQuadRg = ALS_TK_QUAD_RG;
+
+static int topk_nw(int top, bool quad, int rg) {
+  return quad ? tk_nw(kTopQ, rg) : (top <= kTopR ? tk_nw(1) : tk_nw(0));
+}
+
 static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nk = kq / 32;
-  const int nw = (top <= kTopR || quad) ? 8 : 4;
-  const size_t vt = (size_t)tk_vt(nk, nw == 8 ? 1 : 0);
+  const int nw = topk_nw(top, quad, rg);
+  const bool reg_lists = top <= kTopR || quad;
+  const size_t vt = (size_t)tk_vt(nk, reg_lists ? 1 : 0);
   // [2][vt] tile rows of KQ hi halves (stride kq/8 + 2 uint4) | [2][vt] V rows |
   // [2][4] done flags | [4][rg][16] slack coefficients | [4][nk][64] uint4 lo scratch
   const size_t tiles = 16 * 2 * vt * (size_t)(kq / 8 + 2) + 4 * 2 * vt + 4 * 2 * nw +
                        4 * 16 * nw * (size_t)rg + 16 * nw * 64 * (size_t)nk;
-  if (nw == 8) return tiles + sizeof(float) * nw * (size_t)rg * (256 + 16);
+  if (reg_lists) return tiles + sizeof(float) * nw * (size_t)rg * (256 + 16);
   return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +
          sizeof(int) * 64 * (size_t)rg;
 }
@@ -1011,7 +1051,7 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 constexpr int64_t kTkRg2MinRows = 4 * 256 * 256;
 static int topk_split_rg(int k, int top, bool quad, int64_t n_q) {
   const int kq = topk_kq(k);
-  if (quad) return 1;  // quad lists: one row group
+  if (quad) return kTkQuadRg;  // quad lists: one row group, or two (4 wavefronts)
   if (top <= kTopR && n_q < kTkRg2MinRows) return 1;
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
@@ -1095,7 +1135,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
     ALS_LAUNCH_CHECK();
   }
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
-  const int nw = (top <= kTopR || quad) ? tk_nw(1) : tk_nw(0);  // wavefronts per workgroup
+  const int nw = topk_nw(top, quad, rg);  // wavefronts per workgroup
   const unsigned grid = (unsigned)((n_q + 16 * nw * rg - 1) / (16 * nw * rg));
   const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
   const uint4* vlo4 = vsp4 + n_v * (kq / 8);  // lo plane
@@ -1118,16 +1158,16 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
     else if (!quad)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
-    else if (RG != 1)                                 \
+    else if (rg != kTkQuadRg)                         \
       return ALS_EUNSUPPORTED;                        \
     else if (top <= 32)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 32);              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, 32);      \
     else if (top <= 64)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 64);              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, 64);      \
     else if (top <= 100)                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 100);             \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, 100);     \
     else                                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, kTopQ);           \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, kTopQ);   \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);

@@ -11,7 +11,8 @@ def main():
     src = sys.argv[1]
     filt = sys.argv[2] if len(sys.argv) > 2 else ""
     inc = "-I" + os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "recommender-system-using-apache-spark-mllib-_amd", "csrc")
-    p = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", inc,
+    extra = os.environ.get("REGS_FLAGS", "").split()
+    p = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", inc] + extra + [
                         "-c", src, "-o", "/tmp/_regs.o", "-Rpass-analysis=kernel-resource-usage"],
                        capture_output=True, text=True)
     cur = None

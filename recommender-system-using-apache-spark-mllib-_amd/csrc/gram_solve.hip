@@ -52,6 +52,13 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
 constexpr int kRescueGrid = 256;     // waves walking the rescue list (rescue_kernel)
 constexpr int kRescueChunk = 2048;   // fp32 accumulation span of a rescued row
+#ifndef ALS_PERSIST
+#define ALS_PERSIST 0
+#endif
+#ifndef ALS_PERSIST_OCC
+#define ALS_PERSIST_OCC 3
+#endif
+constexpr int kPersistWaves = 256 * 4 * 3 * 2;  // CUs x SIMDs x waves/SIMD x 2
 constexpr int kMaxRank = 128;
 
 template <int CN>
@@ -1803,6 +1810,103 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
   }
 }
 
+// Persistent form of gram_solve_kernel for explicit feedback at k <= 64 (A/B under
+// test, ALS_PERSIST): a grid of resident waves walks the launch-1 task list with a
+// stride (task order is the LPT order, so every wave still meets long rows first),
+// and the next task's schedule entries (light_rows -> row_ptr, or the chunk bounds)
+// are loaded while the current task runs, so the chain of dependent loads that starts
+// every one-task wave is off the critical path.  Same arithmetic as gram_solve_kernel.
+template <int CN>
+__global__ __launch_bounds__(64, ALS_PERSIST_OCC) void gram_solve_persist_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
+    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
+    int32_t n_chunks, int32_t n_light, float* __restrict__ X, int ld, int k, float reg,
+    double* __restrict__ slots, int32_t* __restrict__ status, const float* __restrict__ scal,
+    const uint32_t* __restrict__ Ysp, int32_t kp, int32_t zero_row,
+    unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
+  constexpr int NT = Cfg<CN>::NT;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  const int n_tasks = n_chunks + n_light;
+  int t = blockIdx.x;
+  if (t >= n_tasks) return;
+  const int ey = split_exponent(scal[0]), er = split_exponent(scal[1]);
+  const float inv2 = ldexpf(1.f, -2 * ey);
+  int chunk, light;
+  decode_task(t, n_chunks, n_light, chunk, light);
+  int row = chunk >= 0 ? -1 : light_rows[light];
+  int64_t pb = chunk >= 0 ? chunk_begin[chunk] : row_ptr[row];
+  int64_t pe = chunk >= 0 ? chunk_end[chunk] : row_ptr[row + 1];
+  for (;;) {
+    // the next task's first schedule load, in flight during this task's Gram
+    const int tn = t + (int)gridDim.x;
+    const bool more = tn < n_tasks;
+    int nchunk = -1, nlight = -1, nrow = -1;
+    int64_t npb = 0, npe = 0;
+    if (more) {
+      decode_task(tn, n_chunks, n_light, nchunk, nlight);
+      if (nchunk >= 0) {
+        npb = chunk_begin[nchunk];
+        npe = chunk_end[nchunk];
+      } else {
+        nrow = light_rows[nlight];
+      }
+    }
+    floatx4 acc[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+    float bt[CN];
+    float rmax = 0.f;
+    {
+      floatx4 accb[CN];
+#pragma unroll
+      for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+      gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
+                                         ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
+                                         reinterpret_cast<int*>(smem), rmax);
+      rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
+    }
+    // the next row's bounds, in flight during this task's solve
+    if (more && nchunk < 0) {
+      npb = row_ptr[nrow];
+      npe = row_ptr[nrow + 1];
+    }
+    rmax *= ldexpf(1.f, er);
+    if (chunk >= 0) {
+      float tot[NT][4];
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
+      store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt, rmax);
+    } else if (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax)) {
+      rescue_append(rescue_cnt, rescue_list, row);
+    } else {
+      __syncthreads();  // staging area is reused by the solve
+      if constexpr (CN == 4) {
+        w1_finish_and_solve<false, 4, (bool)ALS_K64_SPLIT>(acc, inv2, bt, pe - pb, nullptr, smem, k,
+                                                           reg, X + (int64_t)row * ld, ld, row,
+                                                           status);
+      } else {
+        float tot[NT][4];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
+        finish_and_solve<CN, false, float>(tot, bt, pe - pb, smem, k, reg, nullptr,
+                                           X + (int64_t)row * ld, ld, row, status);
+      }
+    }
+    if (!more) break;
+    __syncthreads();  // the solve's LDS is reused by the next Gram's staging
+    t = tn;
+    chunk = nchunk;
+    row = nrow;
+    pb = npb;
+    pe = npe;
+  }
+}
+
 __device__ __forceinline__ void block_absmax_publish(float m, unsigned* __restrict__ out) {
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   __shared__ float red[4];
@@ -2718,7 +2822,11 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const bool rescue = (phases & ALS_PHASE_RESCUE) && !implicit && n_rows > 0;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
-    if (g1)                                                                                       \
+    if (g1 && ALS_PERSIST && !IMP)                                                                \
+      gram_solve_persist_kernel<CN><<<std::min<unsigned>(g1, kPersistWaves), 64, 0, st>>>(        \
+          row_ptr, col, val, light_rows, chunk_begin, chunk_end, n_chunks, n_light_primal, X_dst, \
+          ld, k, reg, slots, status_dev, scal, Ysp, kp, zero_row, rescue_cnt, rescue_list);       \
+    else if (g1)                                                                                  \
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
                                                     chunk_begin, chunk_end, n_chunks,             \
                                                     n_light_primal, Y_src, X_dst, ld, k, reg,     \

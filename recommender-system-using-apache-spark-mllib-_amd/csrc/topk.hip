@@ -78,6 +78,9 @@ __global__ __launch_bounds__(256) void tk_absmax_kernel(const float* __restrict_
 }  // namespace
 
 constexpr int kTopkMax = 256;
+#ifndef ALS_TK_BPREF
+#define ALS_TK_BPREF 0
+#endif
 constexpr int kLdsBytes = 160 * 1024;  // per CU on gfx950 (one workgroup may use it all)
 
 // Lists hold (score, index) as one 64-bit key whose unsigned order is the
@@ -650,6 +653,23 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const 
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
     }
   };
+  // One wavefront per SIMD (quad lists, two row groups): no partner wave hides the LDS
+  // latency of the B operands, so they are read one block ahead into registers
+  // (ALS_TK_BPREF, A/B under test).
+  constexpr bool BPREF = QUAD && RG == 2 && ALS_TK_BPREF;
+  auto load_b = [&](const uint4* tb, tk_half8 (&bh)[NK]) {
+#pragma unroll
+    for (int s = 0; s < NK; ++s) bh[s] = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+  };
+  auto score_b = [&](const tk_half8 (&bh)[NK], floatx4 (&acc)[RG]) {
+#pragma unroll
+    for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh[s], acc[g], 0, 0, 0);
+  };
   // + hi.lo + lo.hi.  The lo halves of the block's V rows come from the lo plane in
   // global memory (only blocks past the coarse filter need them), by LDS-DMA into the
   // wave's scratch: each lane reads back the 16 B it loaded, and no VGPR holds them.
@@ -870,17 +890,39 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const 
       if (!wdone) {
         if constexpr (MODE == 3) ++n_tiles;
         floatx4 acc0[RG], acc1[RG];
-        score(tb + m * RS, acc0);
-        // block pairs: issue block c+1's MFMAs, then filter block c
+        if constexpr (BPREF) {
+          // B operands of block c+2 in flight while blocks c, c+1 are scored / filtered
+          static_assert(NC % 2 == 0, "block pairs");
+          tk_half8 bA[NK], bB[NK];
+          load_b(tb + m * RS, bA);
+          load_b(tb + (16 + m) * RS, bB);
+          score_b(bA, acc0);
 #pragma unroll 1
-        for (int c = 0; c < NC; c += 2) {
-          const uint4* tbr = tb + (16 * c + m) * RS;
-          const int* bp = tperm + buf * VT + 16 * c;
-          if (NC > 1) score(tbr + 16 * RS, acc1);
-          filter(acc0, vb + 16 * c, bp, tbr);
-          if (NC > 1) {
-            if (c + 2 < NC) score(tbr + 32 * RS, acc0);
+          for (int c = 0; c < NC; c += 2) {
+            const uint4* tbr = tb + (16 * c + m) * RS;
+            const int* bp = tperm + buf * VT + 16 * c;
+            score_b(bB, acc1);
+            if (c + 2 < NC) load_b(tbr + 32 * RS, bA);
+            filter(acc0, vb + 16 * c, bp, tbr);
+            if (c + 2 < NC) {
+              score_b(bA, acc0);
+              load_b(tbr + 48 * RS, bB);
+            }
             filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
+          }
+        } else {
+          score(tb + m * RS, acc0);
+          // block pairs: issue block c+1's MFMAs, then filter block c
+#pragma unroll 1
+          for (int c = 0; c < NC; c += 2) {
+            const uint4* tbr = tb + (16 * c + m) * RS;
+            const int* bp = tperm + buf * VT + 16 * c;
+            if (NC > 1) score(tbr + 16 * RS, acc1);
+            filter(acc0, vb + 16 * c, bp, tbr);
+            if (NC > 1) {
+              if (c + 2 < NC) score(tbr + 32 * RS, acc0);
+              filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
+            }
           }
         }
       }

@@ -482,6 +482,24 @@ def dual_view(workload: str, k: int, blocks: dict, ms: dict, reg: float):
     return out if out["launches"] else None
 
 
+def rescued_rows(core, k, reg, imp, alpha):
+    """One more (untimed) iteration, reading the rescue list's length before each
+    RESCUE phase: rows the fp32-grade path handed to the fp64 re-solve (split window,
+    pivot spread, failed pivot) per half-sweep — 0 on well-scaled data."""
+    out = {}
+    for name, block, Y, X, n_src in (("item", core.item_block, core.U, core.V, core.n_users),
+                                     ("user", core.user_block, core.V, core.U, core.n_items)):
+        yty = E.compute_yty(Y, n_src, k, core.ws) if imp else None
+        E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
+                     E.PHASE_ALL & ~E.PHASE_RESCUE)
+        torch.cuda.synchronize()
+        out[name] = int(core.ws.buf[8:12].view(torch.int32).item())  # scale word 2
+        E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
+                     E.PHASE_RESCUE)
+    torch.cuda.synchronize()
+    return out
+
+
 def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
     """warmup + `steps` timed iterations from the seeded start; per-iteration wall time
     and the event times of the primal and dual launches of each half-sweep
@@ -510,6 +528,7 @@ def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
     roof = roofline(workload, dominant_kernel(k, imp), launches, k, imp)
     dual = None if imp else dual_view(workload, k, {"item": ib, "user": ub},
                                       {"item": avg(1, 2), "user": avg(4, 5)}, reg)
+    roof["fp64_rescued_rows_per_half_sweep"] = rescued_rows(core, k, reg, imp, alpha)
     return 1e3 * dt, roof, dual
 
 

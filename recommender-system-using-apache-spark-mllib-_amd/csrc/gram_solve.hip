@@ -50,8 +50,13 @@ namespace als {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
-constexpr int kRescueGrid = 256;     // waves walking the rescue list (rescue_kernel)
-constexpr int kRescueChunk = 2048;   // fp32 accumulation span of a rescued row
+constexpr int kRescueGrid = 256;     // workgroups walking the rescue list (rescue64_kernel)
+// Largest LDL^T pivot spread (max / min pivot, a lower bound on cond(A)) the fp32 solve
+// keeps: beyond it the row is re-solved in fp64.  Measured error of the fp32 path is
+// ~3e-7 at the spreads of regularised rating data (lambda 0.1: spread <~ 60); rows
+// with lambda n far below |y|^2 n (short rows at lambda 1e-3, implicit confidences
+// spanning six decades) reach 1e-3..1e-1 in fp32.
+constexpr float kCondMax = 256.f;
 #ifndef ALS_PERSIST
 #define ALS_PERSIST 0
 #endif
@@ -1035,6 +1040,7 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
   for (int c = 0; c < CN; ++c)
     if (q == c) rb = bq[c];
   bool okl = true;  // this lane: every pivot of its diagonal lane was > 0
+  float pmin = 3.0e38f, pmax = 0.f;  // this lane's pivots (lanes < 16)
   static_for<NB>([&](auto Kc) {
     constexpr int K = decltype(Kc)::value;
     constexpr int NCOL = 16 * (NB - K);
@@ -1072,6 +1078,10 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
       myd = put_lane<p>(myd, d);
     });
     okl = okl && (myd > 0.f);  // lanes >= 16 keep myd = 1; NaN pivots fail
+    if (lane < 16 && lane * CN + K < k) {  // pivots of real dims
+      pmin = fminf(pmin, myd);
+      pmax = fmaxf(pmax, myd);
+    }
     // (c) U columns -> tile slots (block row K); z_K, D_K
     if (col_ok) {
 #pragma unroll
@@ -1107,7 +1117,12 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     }
   });
   wave_lds_sync();
-  const bool ok = __ballot(!okl) == 0;
+  // pivot spread (lower bound on cond(A)) within what fp32 holds to the 1e-4 bar
+  for (int o = 32; o > 0; o >>= 1) {
+    pmin = fminf(pmin, __shfl_xor(pmin, o));
+    pmax = fmaxf(pmax, __shfl_xor(pmax, o));
+  }
+  const bool ok = __ballot(!okl) == 0 && pmax <= kCondMax * pmin;
   // (e) back substitution
   block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);
   // (f) un-permute: dim d = i*CN + K  <->  Xv[K*16 + i]
@@ -1222,7 +1237,8 @@ __device__ __forceinline__ float reduce_lanes16(float v) {
 // hook(p) runs after pivot p: the caller interleaves independent matrix-core work
 // there (the asm statements fix the instruction order).
 template <class Hook>
-__device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook) {
+__device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& rmin, float& rmax,
+                                        int preal) {
   float dmin = 3.0e38f;  // NaN pivots are not seen here: they make the solution NaN
   float dself = 1.f;     // this lane's own pivot (its column's deferred scale is 1/dself)
   // pivot p's broadcast pivot, reciprocal and multipliers; for p > 0 they are formed
@@ -1235,6 +1251,10 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook) {
   static_for<16>([&](auto pc) {
     constexpr int p = decltype(pc)::value;
     dmin = fminf(dmin, d);
+    if (p < preal) {  // the pivots of real (not padded) dims: their spread
+      rmin = fminf(rmin, d);
+      rmax = fmaxf(rmax, d);
+    }
     // R[i] += (lane p's R[i]) * nf as ONE v_fmac_f32_dpp per row (the compiler only
     // folds DPP into untied VOP2 ops); s_nop 1 covers the VALU-write -> DPP-read
     // hazard of the previous pivot's last writes.
@@ -1297,7 +1317,8 @@ __device__ __forceinline__ float sel_mask(float v, float w) {
 // entry sees the same fp32 operations, in the same order, as in sweep16 (deferred
 // pivot-column scaling, look-ahead of the next pivot).
 template <class Hook>
-__device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook) {
+__device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& rmin, float& rmax,
+                                         int preal) {
   float B[4] = {Bv[0], Bv[1], Bv[2], Bv[3]};
   float dmin = 3.0e38f;
   float dself = 1.f;
@@ -1310,6 +1331,10 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook) {
     constexpr int p = decltype(pc)::value;
     constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
     dmin = fminf(dmin, d);
+    if (p < preal) {  // the pivots of real (not padded) dims: their spread
+      rmin = fminf(rmin, d);
+      rmax = fmaxf(rmax, d);
+    }
     asm volatile("s_nop 1" ::: "memory");
     // the register holding row p+1 first: then pivot p+1's row is final
     fmac_bcast16<p>(B[rn], nf);
@@ -1429,9 +1454,9 @@ __device__ __forceinline__ float absmax4(const floatx4& x) {
 //   max diag(G) < n T^2  (covers every row whose largest |t| < T: diag <= n max t^2)
 //   or 0 < max |r| < T   (the row's ratings, scaled by the launch's rating scale).
 // A row that misses the window is not solved here: it is appended to the rescue
-// list and re-solved by rescue_kernel with a scale of its own (fp32 rows split in
-// registers after a per-row power of two, rhs in fp32).  Implicit rows need no
-// guard: their A includes YtY (>= the largest row's square) and b is fp32.
+// list and re-solved in fp64 by rescue64_kernel (as are rows whose fp32 LDL^T pivots
+// spread beyond kCondMax, or fail).  Implicit rows need no window test: their A
+// includes YtY (>= the largest row's square) and b is fp32.
 // ---------------------------------------------------------------------------
 constexpr float kWindowT = 0.0625f;  // 2^-4, in scaled units (launch max in [2^14, 2^15))
 
@@ -1500,6 +1525,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   float* vec = lds + L::VEC;
   float zcol[NB];
   float dmin = 3.0e38f;
+  float rmin = 3.0e38f, rmax = 0.f;  // pivots of the real dims (dims < k)
   if constexpr (SPLIT) {
     // scale the system by 2^g: largest diagonal entry (= largest entry) -> [2^13, 2^14)
     float dm = 0.f;
@@ -1533,7 +1559,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
     if constexpr (ALS_SWEEP_C) {
       // swept in the C layout: Gm comes out where the MFMAs read it
       Gm = A[w1_tile<NB>(K, K)];
-      dmin = fminf(dmin, sweep16c(Gm, hook));
+      dmin = fminf(dmin, sweep16c(Gm, hook, rmin, rmax, (k - K + NB - 1) / NB));
       const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
       if (q == 0) vec[m] = bK;
       wave_lds_order();
@@ -1548,7 +1574,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
         const floatx4 v = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * c4);
         R[4 * c4] = v[0]; R[4 * c4 + 1] = v[1]; R[4 * c4 + 2] = v[2]; R[4 * c4 + 3] = v[3];
       }
-      dmin = fminf(dmin, sweep16(R, hook));
+      dmin = fminf(dmin, sweep16(R, hook, rmin, rmax, (k - K + NB - 1) / NB));
       wave_lds_order();
       const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
       if (q == 0) {
@@ -1668,11 +1694,13 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
     xcol[K] = zcol[K] + vec[m];
     wave_lds_order();
   });
-  // a NaN pivot (or overflow) leaves a non-finite solution
+  // a NaN pivot (or overflow) leaves a non-finite solution; a pivot spread beyond
+  // kCondMax (a lower bound on cond(A)) is outside what the fp32 solve can hold to the
+  // 1e-4 bar: the row is re-solved in fp64 (rescue64_kernel)
   bool fin = true;
 #pragma unroll
   for (int c = 0; c < NB; ++c) fin = fin && (xcol[c] - xcol[c] == 0.f);
-  return dmin > 0.f && __ballot(!fin) == 0;
+  return dmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;
 }
 
 // w1_solve_x, then the solution row written un-permuted: dim d = i * NB + c <->
@@ -1717,7 +1745,8 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
                                                  int64_t n_reg, unsigned char* smem, int k,
                                                  float reg, const double* __restrict__ yty,
                                                  float* __restrict__ xrow, int ld, int row,
-                                                 int32_t* __restrict__ status) {
+                                                 unsigned* __restrict__ rescue_cnt,
+                                                 int32_t* __restrict__ rescue_list) {
   constexpr int NT = Cfg<CN>::NT;
   float bq[CN];
   const int m = threadIdx.x & 15;
@@ -1753,7 +1782,7 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
   }
   regularise_f32<CN>(A, (float)((double)reg * (double)n_reg), k);
   const bool ok = panel_ldl_solve<CN>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
-  if (!ok && (threadIdx.x & 63) == 0) atomicCAS(status, 0, row + 1);
+  if (!ok) rescue_append(rescue_cnt, rescue_list, row);  // re-solved in fp64
 }
 
 // Partial-sum slot of one task: N tiles x 4 accumulator rows, NRA rhs values and
@@ -1812,7 +1841,8 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
-                                                    int32_t* __restrict__ status);
+                                                    unsigned* __restrict__ rescue_cnt,
+                                                    int32_t* __restrict__ rescue_list);
 
 // (k <= 64 keeps one gather step in flight: two steps need 187 registers, i.e. two
 // waves per SIMD instead of three, measured slower on configs[1]: 2.07 -> 2.24 ms/iter.)
@@ -1888,10 +1918,10 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     // inverses + fp32 MFMA), in the Gram's scale
     static_assert(W1LdsT<4>::SIZE <= PanelLds<4>::SIZE, "W1<4> LDS");
     w1_finish_and_solve<false, 4, (bool)ALS_K64_SPLIT>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
-                                  X + (int64_t)row * ld, ld, row, status);
+                                  X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
   } else {
     finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty,
-                                          X + (int64_t)row * ld, ld, row, status);
+                                          X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
   }
 }
 
@@ -1971,7 +2001,7 @@ __global__ __launch_bounds__(64, ALS_PERSIST_OCC) void gram_solve_persist_kernel
       if constexpr (CN == 4) {
         w1_finish_and_solve<false, 4, (bool)ALS_K64_SPLIT>(acc, inv2, bt, pe - pb, nullptr, smem, k,
                                                            reg, X + (int64_t)row * ld, ld, row,
-                                                           status);
+                                                           rescue_cnt, rescue_list);
       } else {
         float tot[NT][4];
 #pragma unroll
@@ -1979,7 +2009,7 @@ __global__ __launch_bounds__(64, ALS_PERSIST_OCC) void gram_solve_persist_kernel
 #pragma unroll
           for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
         finish_and_solve<CN, false, float>(tot, bt, pe - pb, smem, k, reg, nullptr,
-                                           X + (int64_t)row * ld, ld, row, status);
+                                           X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
       }
     }
     if (!more) break;
@@ -2098,7 +2128,7 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     }
   }
   finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
-                                         X + (int64_t)row * ld, ld, row, status);
+                                         X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
 }
 
 // ---------------------------------------------------------------------------
@@ -2143,7 +2173,8 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
-                                                    int32_t* __restrict__ status) {
+                                                    unsigned* __restrict__ rescue_cnt,
+                                                    int32_t* __restrict__ rescue_list) {
   constexpr int NT_ = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   const float inv = 1.f / scale;  // power of two: exact
@@ -2184,7 +2215,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
     });
   }
   const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
-  if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
+  if (!ok) rescue_append(rescue_cnt, rescue_list, row);  // re-solved in fp64
 }
 
 // Launch 1 (W1): heavy-row chunks (-> fp32 partial slots) and whole light rows
@@ -2264,7 +2295,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
   w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT || (bool)ALS_W1E_SPLIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
-                                               X + (int64_t)row * ld, ld, row, status);
+                                               X + (int64_t)row * ld, ld, row, rescue_cnt,
+                                               rescue_list);
 }
 
 // ---------------------------------------------------------------------------
@@ -2397,7 +2429,10 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
 #pragma unroll
   for (int c = 0; c < NB; ++c) bcol[c] = rc[c] * inv;
   const bool ok = w1_solve_x<NB, (bool)ALS_DUAL_SPLIT>(acc, bcol, lds, n, z);
-  if (!ok && lane == 0) atomicCAS(status, 0, row + 1);
+  if (!ok) {  // re-solved in fp64 (the primal k x k system)
+    rescue_append(rescue_cnt, rescue_list, row);
+    return;
+  }
   // x = Y_S^T z: z split into f16 hi + lo after a power-of-two scale
   float zm = 0.f;
 #pragma unroll
@@ -2569,84 +2604,144 @@ __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
     }
   }
   w1_finish_and_solve<false>(A, 1.f, bt, n_reg, nullptr, smem, k, reg, X + (int64_t)row * ld, ld,
-                             row, status);
+                             row, rescue_cnt, rescue_list);
 }
 
-// Rescue launch: the rows whose operands missed the split window (window_miss)
-// are re-solved with a scale of their own.  One wavefront per listed row (a grid
-// of a few hundred waves walks the list; an empty list costs one launch): the
-// row's max |y| over its source rows sets a per-row power of two, the fp32 rows
-// are split in registers after it (gram_accumulate_split, the implicit kernels'
-// loop with weight 1), the rhs is accumulated in fp32 on the VALU, fp32 within
-// `chunk` ratings and fp64 across chunks (LDS, lane-private), then the same
-// finish + solve as the primal kernels.  Any row length (heavy rows included).
-template <int CN>
-__global__ __launch_bounds__(64, 1) void rescue_kernel(
+// Rescue launch: every row the fp32-grade path did not solve to the 1e-4 bar — its
+// operands missed the split window (window_miss), its LDL^T pivots spread beyond
+// kCondMax, or a pivot was not positive / the solution not finite — is re-solved with
+// Spark's own arithmetic: the normal equations accumulated in fp64 from the fp32 factor
+// rows (NormalEquation.add's dspr / daxpy: products of fp32 values are exact in fp64),
+// implicit YtY merged in fp64, lambda * numExplicits on the diagonal, and a fp64
+// Cholesky (dppsv) of the packed lower triangle in LDS.  A pivot that is not positive
+// in fp64 either is Spark's failure: status = row + 1.  One 256-thread workgroup per
+// listed row (a few hundred workgroups walk the list; an empty list costs one launch).
+constexpr int kRescueThreads = 256;
+constexpr int kRescueBatch = 32;  // ratings staged per step
+
+// (i, j), i >= j, of lower-packed entry e (e = i (i + 1) / 2 + j).
+__device__ __forceinline__ void packed_ij(int e, int& i, int& j) {
+  int r = (int)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= e) ++r;
+  while (r * (r + 1) / 2 > e) --r;
+  i = r;
+  j = e - r * (r + 1) / 2;
+}
+
+template <bool IMPLICIT>
+__global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, const float* __restrict__ Y, float* __restrict__ X, int ld,
-    int k, float reg, int32_t* __restrict__ status, const unsigned* __restrict__ rescue_cnt,
-    const int32_t* __restrict__ rescue_list, int chunk) {
-  constexpr int NT = Cfg<CN>::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
-  __shared__ double a64s[NT * 4 * 64];
-  __shared__ double b64s[CN * 64];
-  const int lane = threadIdx.x & 63;
+    const float* __restrict__ val, const float* __restrict__ Y, int ld, int k, float reg,
+    float alpha, const double* __restrict__ yty, float* __restrict__ X,
+    int32_t* __restrict__ status, const unsigned* __restrict__ rescue_cnt,
+    const int32_t* __restrict__ rescue_list) {
+  constexpr int NPMAX = kMaxRank * (kMaxRank + 1) / 2;
+  __shared__ double Ap[NPMAX];  // lower-packed A
+  __shared__ double bs[kMaxRank];
+  __shared__ float ys[kRescueBatch][kMaxRank + 1];
+  __shared__ double wa[kRescueBatch], wb[kRescueBatch];
+  __shared__ int npos_s;
+  __shared__ int fail_s;
+  const int tid = threadIdx.x;
+  const int np = k * (k + 1) / 2;
   const unsigned n_list = *rescue_cnt;
   for (unsigned it = blockIdx.x; it < n_list; it += gridDim.x) {
     const int row = rescue_list[it];
     const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
-    float mx = 0.f;
-    for (int64_t e = pb + lane; e < pe; e += 64) {
-      const float* yr = Y + (int64_t)col[e] * ld;
-      for (int d = 0; d < k; ++d) mx = fmaxf(mx, __builtin_fabsf(yr[d]));
+    for (int e = tid; e < np; e += kRescueThreads) Ap[e] = IMPLICIT ? yty[e] : 0.0;
+    for (int d = tid; d < k; d += kRescueThreads) bs[d] = 0.0;
+    if (tid == 0) {
+      npos_s = 0;
+      fail_s = 0;
     }
-    const int ex = split_exponent(wave_max(mx));
-    const double inv2 = ldexp(1.0, -2 * ex);
-    for (int t = 0; t < NT * 4; ++t) a64s[t * 64 + lane] = 0.0;
-    for (int c = 0; c < CN; ++c) b64s[c * 64 + lane] = 0.0;
-    for (int64_t c0 = pb; c0 < pe; c0 += chunk) {
-      const int64_t c1 = c0 + chunk < pe ? c0 + chunk : pe;
-      floatx4 acc[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-      float bf[CN];
-#pragma unroll
-      for (int c = 0; c < CN; ++c) bf[c] = 0.f;
-      int npos = 0;
-      gram_accumulate_split<CN, false>(col, val, c0, c1, Y, ld, k, 0.f, ldexpf(1.f, ex), acc, bf,
-                                       npos, reinterpret_cast<int*>(smem));
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a64s[(t * 4 + r) * 64 + lane] += (double)acc[t][r] * inv2;
-#pragma unroll
-      for (int c = 0; c < CN; ++c) b64s[c * 64 + lane] += (double)bf[c];
-      wave_lds_sync();
+    __syncthreads();
+    int npos = 0;
+    for (int64_t base = pb; base < pe; base += kRescueBatch) {
+      const int nb = (int)(pe - base < kRescueBatch ? pe - base : kRescueBatch);
+      if (tid < kRescueBatch) {
+        const bool v = tid < nb;
+        const double r = v ? (double)val[base + tid] : 0.0;
+        if (IMPLICIT) {
+          const double c1 = (double)alpha * fabs(r);
+          wa[tid] = v ? c1 : 0.0;
+          wb[tid] = (v && r > 0.0) ? 1.0 + c1 : 0.0;
+          npos += (v && r > 0.0) ? 1 : 0;
+        } else {
+          wa[tid] = v ? 1.0 : 0.0;
+          wb[tid] = r;
+        }
+      }
+      for (int x = tid; x < kRescueBatch * k; x += kRescueThreads) {
+        const int jr = x / k, d = x - jr * k;
+        ys[jr][d] = jr < nb ? Y[(int64_t)col[base + jr] * ld + d] : 0.f;
+      }
+      __syncthreads();
+      for (int e = tid; e < np; e += kRescueThreads) {
+        int i, j;
+        packed_ij(e, i, j);
+        double acc = 0.0;
+        for (int jr = 0; jr < nb; ++jr)
+          acc = fma(wa[jr], (double)ys[jr][i] * (double)ys[jr][j], acc);
+        Ap[e] += acc;
+      }
+      for (int d = tid; d < k; d += kRescueThreads) {
+        double acc = 0.0;
+        for (int jr = 0; jr < nb; ++jr) acc = fma(wb[jr], (double)ys[jr][d], acc);
+        bs[d] += acc;
+      }
+      __syncthreads();
     }
+    if (IMPLICIT && tid < kRescueBatch) atomicAdd(&npos_s, npos);
+    __syncthreads();
+    const double lam = (double)reg * (double)(IMPLICIT ? npos_s : (int)(pe - pb));
+    for (int d = tid; d < k; d += kRescueThreads) Ap[d * (d + 1) / 2 + d] += lam;
+    __syncthreads();
+    // Cholesky A = L L^T (right-looking, packed lower, in place)
+    for (int jc = 0; jc < k; ++jc) {
+      const int dj = jc * (jc + 1) / 2 + jc;
+      const double dd = Ap[dj];
+      if (!(dd > 0.0)) {  // uniform: every thread reads the same value
+        if (tid == 0) fail_s = 1;
+        break;
+      }
+      const double l = sqrt(dd);
+      __syncthreads();
+      if (tid == 0) Ap[dj] = l;
+      for (int i = jc + 1 + tid; i < k; i += kRescueThreads) Ap[i * (i + 1) / 2 + jc] /= l;
+      __syncthreads();
+      const int m = k - jc - 1;  // trailing block, lower-packed entries (a, c), c <= a
+      for (int t = tid; t < m * (m + 1) / 2; t += kRescueThreads) {
+        int a, c;
+        packed_ij(t, a, c);
+        const int ia = jc + 1 + a, ic = jc + 1 + c;
+        Ap[ia * (ia + 1) / 2 + ic] -= Ap[ia * (ia + 1) / 2 + jc] * Ap[ic * (ic + 1) / 2 + jc];
+      }
+      __syncthreads();
+    }
+    __syncthreads();
     float* xrow = X + (int64_t)row * ld;
-    if constexpr (CN <= 2) {
-      double a64[NT][4], bb[CN];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) a64[t][r] = a64s[(t * 4 + r) * 64 + lane];
-#pragma unroll
-      for (int c = 0; c < CN; ++c) bb[c] = b64s[c * 64 + lane];
-      finish_and_solve<CN, false, double>(a64, bb, pe - pb, smem, k, reg, nullptr, xrow, ld, row,
-                                          status);
+    if (fail_s) {
+      if (tid == 0) atomicCAS(status, 0, row + 1);  // Spark: dppsv info > 0
+      for (int d = tid; d < ld; d += kRescueThreads) xrow[d] = 0.f;
     } else {
-      floatx4 A[NT];
-      float bt[CN];
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) A[t][r] = (float)a64s[(t * 4 + r) * 64 + lane];
-#pragma unroll
-      for (int c = 0; c < CN; ++c) bt[c] = (float)b64s[c * 64 + lane];
-      w1_finish_and_solve<false, CN, CN == 8>(A, 1.f, bt, pe - pb, nullptr, smem, k, reg, xrow,
-                                              ld, row, status);
+      // L y = b (forward), L^T x = y (backward), column-oriented
+      for (int jc = 0; jc < k; ++jc) {
+        const double yj = bs[jc] / Ap[jc * (jc + 1) / 2 + jc];
+        __syncthreads();
+        if (tid == 0) bs[jc] = yj;
+        for (int i = jc + 1 + tid; i < k; i += kRescueThreads) bs[i] -= Ap[i * (i + 1) / 2 + jc] * yj;
+        __syncthreads();
+      }
+      for (int jc = k - 1; jc >= 0; --jc) {
+        const double xj = bs[jc] / Ap[jc * (jc + 1) / 2 + jc];
+        __syncthreads();
+        if (tid == 0) bs[jc] = xj;
+        for (int i = tid; i < jc; i += kRescueThreads) bs[i] -= Ap[jc * (jc + 1) / 2 + i] * xj;
+        __syncthreads();
+      }
+      for (int d = tid; d < ld; d += kRescueThreads) xrow[d] = d < k ? (float)bs[d] : 0.f;
     }
-    __syncthreads();  // smem reused by the next listed row
+    __syncthreads();  // LDS reused by the next listed row
   }
 }
 
@@ -2904,7 +2999,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const unsigned g1 = (phases & ALS_PHASE_LAUNCH1) ? (unsigned)(n_chunks + n_light_primal) : 0u;
   const unsigned gd = (phases & ALS_PHASE_DUAL) ? (unsigned)(n_light - n_light_primal) : 0u;
   const unsigned g2 = (phases & ALS_PHASE_LAUNCH2) ? (unsigned)n_heavy : 0u;
-  const bool rescue = (phases & ALS_PHASE_RESCUE) && !implicit && n_rows > 0;
+  const bool rescue = (phases & ALS_PHASE_RESCUE) && n_rows > 0;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
     if (g1 && ALS_PERSIST && !IMP)                                                                \
@@ -2935,9 +3030,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
     if (rescue) {                                                                                 \
-      rescue_kernel<CN><<<kRescueGrid, 64, 0, st>>>(row_ptr, col, val, Y_src, X_dst, ld, k, reg,  \
-                                                    status_dev, rescue_cnt, rescue_list,          \
-                                                    kRescueChunk);                                \
+      rescue64_kernel<IMP><<<kRescueGrid, kRescueThreads, 0, st>>>(                               \
+          row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rescue_cnt, \
+          rescue_list);                                                                           \
       ALS_LAUNCH_CHECK();                                                                         \
       ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));                               \
     }                                                                                             \
@@ -2969,9 +3064,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
     if (rescue) {                                                                                 \
-      rescue_kernel<8><<<kRescueGrid, 64, 0, st>>>(row_ptr, col, val, Y_src, X_dst, ld, k, reg,   \
-                                                   status_dev, rescue_cnt, rescue_list,           \
-                                                   kRescueChunk);                                 \
+      rescue64_kernel<IMP><<<kRescueGrid, kRescueThreads, 0, st>>>(                               \
+          row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rescue_cnt, \
+          rescue_list);                                                                           \
       ALS_LAUNCH_CHECK();                                                                         \
       ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));                               \
     }                                                                                             \

@@ -51,12 +51,12 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
 constexpr int kRescueGrid = 256;     // workgroups walking the rescue list (rescue64_kernel)
-// Largest LDL^T pivot spread (max / min pivot, a lower bound on cond(A)) the fp32 solve
-// keeps: beyond it the row is re-solved in fp64.  Measured error of the fp32 path is
-// ~3e-7 at the spreads of regularised rating data (lambda 0.1: spread <~ 60); rows
-// with lambda n far below |y|^2 n (short rows at lambda 1e-3, implicit confidences
-// spanning six decades) reach 1e-3..1e-1 in fp32.
-constexpr float kCondMax = 256.f;
+// Largest LDL^T pivot spread (max / min pivot of the real dims, a lower bound on
+// cond(A)) the fp32 solve keeps: beyond it the row is re-solved in fp64.  Regularised
+// rating data (lambda 0.1) spread far less (pivots lie in [lambda_min, lambda_max] and
+// the diagonal stays within a few times lambda n); implicit confidences spanning six
+// decades spread by 1e3-1e5 and reach 1e-3 errors in fp32.
+constexpr float kCondMax = 32.f;
 #ifndef ALS_PERSIST
 #define ALS_PERSIST 0
 #endif
@@ -1473,6 +1473,33 @@ __device__ __forceinline__ float diag_max_lane(const floatx4 (&A)[CN * (CN + 1) 
   return d;
 }
 
+// Sum of the diagonal entries of real dims (dims < k) of an upper-tile set in the C
+// layout, summed over the wave (every lane gets it).
+template <int CN>
+__device__ __forceinline__ float diag_trace(const floatx4 (&A)[CN * (CN + 1) / 2], int k) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  float t = 0.f;
+#pragma unroll
+  for (int c = 0; c < CN; ++c)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * q + r == m && m * CN + c < k) t += A[tile_index(CN, c, c)][r];
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  return t;
+}
+
+// Rank-deficient rows (n < 2k ratings, explicit): A = G + lambda n I has
+// lambda_min >= lambda n and lambda_max <= tr(G) + lambda n, so cond(A) <= 1 + tr(G) /
+// (lambda n).  With G of low rank the fp32 solve's error grows as that bound (measured
+// ~1.5e-6 x tr(G) / (lambda n) at n << k), which the LDL^T pivots do not show (they stay
+// within (tr(G)/k + lambda n) / (lambda n)).  Beyond kCondRankDef the row is re-solved
+// in fp64.  tr_scaled: tr(G) in the Gram's scale (x 1/inv2).
+constexpr float kCondRankDef = 64.f;
+__device__ __forceinline__ bool rank_deficient_illcond(float tr_scaled, float inv2, int64_t n, int k,
+                                                       float reg) {
+  return n < 2 * (int64_t)k && tr_scaled * inv2 > (kCondRankDef - 1.f) * reg * (float)n;
+}
+
 // Wave-uniform: do the scaled operands of a task with n terms miss the window?
 __device__ __forceinline__ bool window_miss(float diag_lane, float n_terms, float rmax_lane) {
   const float d = wave_max(diag_lane), r = wave_max(rmax_lane);
@@ -1895,7 +1922,8 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
                                        reinterpret_cast<int*>(smem), rmax);
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
     rmax *= ldexpf(1.f, er);
-    if (chunk < 0 && window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax)) {
+    if (chunk < 0 && (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
+                      rank_deficient_illcond(diag_trace<CN>(acc, k), inv2, pe - pb, k, reg))) {
       rescue_append(rescue_cnt, rescue_list, row);
       return;
     }
@@ -1994,7 +2022,8 @@ __global__ __launch_bounds__(64, ALS_PERSIST_OCC) void gram_solve_persist_kernel
 #pragma unroll
         for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
       store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt, rmax);
-    } else if (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax)) {
+    } else if (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
+               rank_deficient_illcond(diag_trace<CN>(acc, k), inv2, pe - pb, k, reg)) {
       rescue_append(rescue_cnt, rescue_list, row);
     } else {
       __syncthreads();  // staging area is reused by the solve
@@ -2275,7 +2304,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
                                          reinterpret_cast<int*>(smem), rmax);
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
     rmax *= ldexpf(1.f, er);
-    if (chunk < 0 && window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax)) {
+    if (chunk < 0 && (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
+                      rank_deficient_illcond(diag_trace<CN>(acc, k), inv2, pe - pb, k, reg))) {
       rescue_append(rescue_cnt, rescue_list, row);
       return;
     }

@@ -340,6 +340,16 @@ def _probe_spark():
     return {"java": java, "pyspark": pys}
 
 
+def _cgroup_cpus():
+    """CPUs' worth of time the cgroup v2 quota allows (None: no quota)."""
+    c = _cgroup_cpu_max()
+    try:
+        q, per = c.split()
+        return None if q == "max" else max(1, -(-int(q) // int(per)))
+    except Exception:
+        return None
+
+
 def _cgroup_cpu_max():
     """The cgroup v2 CPU quota of this process ("max 100000" = none), if readable."""
     try:
@@ -356,12 +366,17 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
     import numpy as np
     from oracle import c_oracle
     # every core this process may run on ("N = all host cores"), passed
-    # explicitly to the OpenMP port (OMP_NUM_THREADS is left as the host set it)
+    # explicitly to the OpenMP port (OMP_NUM_THREADS is left as the host set it) ...
     try:
         affinity = len(os.sched_getaffinity(0))
     except Exception:
         affinity = None
-    threads = affinity or os.cpu_count()
+    # ... but a cgroup CPU quota caps the CPU time of the whole process: on the GPU box
+    # "1600000 100000" = 16 CPUs' worth over a 256-CPU affinity mask, where 256 threads
+    # only time-slice (measured: 8.6e6 ratings/s with 256 threads vs 1.9e7 with 16).
+    # threads = the CPUs this process can actually use: min(affinity, quota).
+    quota = _cgroup_cpus()
+    threads = min(affinity or os.cpu_count(), quota or 1 << 30)
     U = core.U[:, :rank].contiguous().cpu().numpy()
     V = core.V[:, :rank].contiguous().cpu().numpy()
     total_t = 0.0
@@ -390,7 +405,7 @@ def cpu_baseline(core: "E.ALSCore", rank: int, reg: float, budget_s: float = 12.
     return {"value": core.nnz / total_t, "unit": "ratings/s", "cores": threads, "kind": "port",
             "host_cores": os.cpu_count(), "affinity_cores": affinity, "spark_probe": probe,
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
-            "cgroup_cpu_max": _cgroup_cpu_max(),
+            "cgroup_cpu_max": _cgroup_cpu_max(), "cgroup_cpus": quota,
             "sample": "oracle/als_oracle.c (Spark dspr+dppsv restated, fp64, OpenMP, "
                       f"{threads} threads) on a row prefix of each side; "
                       + "; ".join(sample_desc)

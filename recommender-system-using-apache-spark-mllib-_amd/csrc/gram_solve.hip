@@ -1237,8 +1237,7 @@ __device__ __forceinline__ float reduce_lanes16(float v) {
 // hook(p) runs after pivot p: the caller interleaves independent matrix-core work
 // there (the asm statements fix the instruction order).
 template <class Hook>
-__device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& rmin, float& rmax,
-                                        int preal) {
+__device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& dself_out) {
   float dmin = 3.0e38f;  // NaN pivots are not seen here: they make the solution NaN
   float dself = 1.f;     // this lane's own pivot (its column's deferred scale is 1/dself)
   // pivot p's broadcast pivot, reciprocal and multipliers; for p > 0 they are formed
@@ -1251,10 +1250,6 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& rmi
   static_for<16>([&](auto pc) {
     constexpr int p = decltype(pc)::value;
     dmin = fminf(dmin, d);
-    if (p < preal) {  // the pivots of real (not padded) dims: their spread
-      rmin = fminf(rmin, d);
-      rmax = fmaxf(rmax, d);
-    }
     // R[i] += (lane p's R[i]) * nf as ONE v_fmac_f32_dpp per row (the compiler only
     // folds DPP into untied VOP2 ops); s_nop 1 covers the VALU-write -> DPP-read
     // hazard of the previous pivot's last writes.
@@ -1285,6 +1280,7 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& rmi
   const float s = rcp_t(dself);
 #pragma unroll
   for (int i = 0; i < 16; ++i) R[i] *= s;
+  dself_out = dself;
   return dmin;
 }
 
@@ -1317,8 +1313,7 @@ __device__ __forceinline__ float sel_mask(float v, float w) {
 // entry sees the same fp32 operations, in the same order, as in sweep16 (deferred
 // pivot-column scaling, look-ahead of the next pivot).
 template <class Hook>
-__device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& rmin, float& rmax,
-                                         int preal) {
+__device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
   float B[4] = {Bv[0], Bv[1], Bv[2], Bv[3]};
   float dmin = 3.0e38f;
   float dself = 1.f;
@@ -1331,10 +1326,6 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& rmin,
     constexpr int p = decltype(pc)::value;
     constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
     dmin = fminf(dmin, d);
-    if (p < preal) {  // the pivots of real (not padded) dims: their spread
-      rmin = fminf(rmin, d);
-      rmax = fmaxf(rmax, d);
-    }
     asm volatile("s_nop 1" ::: "memory");
     // the register holding row p+1 first: then pivot p+1's row is final
     fmac_bcast16<p>(B[rn], nf);
@@ -1360,6 +1351,7 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& rmin,
   const float s = rcp_t(dself);
 #pragma unroll
   for (int r = 0; r < 4; ++r) Bv[r] = B[r] * s;
+  dself_out = dself;
   return dmin;
 }
 
@@ -1488,16 +1480,19 @@ __device__ __forceinline__ float diag_trace(const floatx4 (&A)[CN * (CN + 1) / 2
   return t;
 }
 
-// Rank-deficient rows (n < 2k ratings, explicit): A = G + lambda n I has
-// lambda_min >= lambda n and lambda_max <= tr(G) + lambda n, so cond(A) <= 1 + tr(G) /
-// (lambda n).  With G of low rank the fp32 solve's error grows as that bound (measured
-// ~1.5e-6 x tr(G) / (lambda n) at n << k), which the LDL^T pivots do not show (they stay
-// within (tr(G)/k + lambda n) / (lambda n)).  Beyond kCondRankDef the row is re-solved
-// in fp64.  tr_scaled: tr(G) in the Gram's scale (x 1/inv2).
+// Very short explicit rows on the primal path (n <= k / 4 ratings; at k > 32 such rows
+// take the dual path unless it is off): A = G + lambda n I with G of rank n << k has
+// lambda_min = lambda n and lambda_max ~ tr(G) + lambda n, so cond(A) ~ 1 + tr(G) /
+// (lambda n), which the LDL^T pivots do not show (they stay within (tr(G) / k + lambda
+// n) / (lambda n)).  The fp32 solve's error there grows as that bound (measured ~1.5e-6
+// x tr(G) / (lambda n) at n <= 16, k 65-128, lambda 1e-3 / 1e-4; at n > k / 4 the
+// measured errors stay ~1e-5 and below, e.g. 8.8e-7 on the configs[3] users of 97-255
+// ratings).  Beyond kCondRankDef the row is re-solved in fp64.  tr_scaled: tr(G) in the
+// Gram's scale (x 1/inv2).
 constexpr float kCondRankDef = 64.f;
 __device__ __forceinline__ bool rank_deficient_illcond(float tr_scaled, float inv2, int64_t n, int k,
                                                        float reg) {
-  return n < 2 * (int64_t)k && tr_scaled * inv2 > (kCondRankDef - 1.f) * reg * (float)n;
+  return 4 * n <= (int64_t)k && tr_scaled * inv2 > (kCondRankDef - 1.f) * reg * (float)n;
 }
 
 // Wave-uniform: do the scaled operands of a task with n terms miss the window?
@@ -1552,7 +1547,12 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   float* vec = lds + L::VEC;
   float zcol[NB];
   float dmin = 3.0e38f;
-  float rmin = 3.0e38f, rmax = 0.f;  // pivots of the real dims (dims < k)
+  // this lane's pivots of real dims (its column m of every block: dim m * NB + K < k)
+  float rmin = 3.0e38f, rmax = 0.f;
+  auto track_pivot = [&](float ds, bool real) {
+    rmin = real ? fminf(rmin, ds) : rmin;
+    rmax = real ? fmaxf(rmax, ds) : rmax;
+  };
   if constexpr (SPLIT) {
     // scale the system by 2^g: largest diagonal entry (= largest entry) -> [2^13, 2^14)
     float dm = 0.f;
@@ -1586,7 +1586,9 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
     if constexpr (ALS_SWEEP_C) {
       // swept in the C layout: Gm comes out where the MFMAs read it
       Gm = A[w1_tile<NB>(K, K)];
-      dmin = fminf(dmin, sweep16c(Gm, hook, rmin, rmax, (k - K + NB - 1) / NB));
+      float ds;
+      dmin = fminf(dmin, sweep16c(Gm, hook, ds));
+      track_pivot(ds, m * NB + K < k);
       const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
       if (q == 0) vec[m] = bK;
       wave_lds_order();
@@ -1601,7 +1603,9 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
         const floatx4 v = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * c4);
         R[4 * c4] = v[0]; R[4 * c4 + 1] = v[1]; R[4 * c4 + 2] = v[2]; R[4 * c4 + 3] = v[3];
       }
-      dmin = fminf(dmin, sweep16(R, hook, rmin, rmax, (k - K + NB - 1) / NB));
+      float ds;
+      dmin = fminf(dmin, sweep16(R, hook, ds));
+      track_pivot(ds, m * NB + K < k);
       wave_lds_order();
       const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
       if (q == 0) {
@@ -1727,6 +1731,15 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   bool fin = true;
 #pragma unroll
   for (int c = 0; c < NB; ++c) fin = fin && (xcol[c] - xcol[c] == 0.f);
+  // spread over the 16 lanes of a row group (every row group holds the same pivots)
+  rmin = fminf(rmin, dpp_f<0xB1>(rmin));
+  rmax = fmaxf(rmax, dpp_f<0xB1>(rmax));
+  rmin = fminf(rmin, dpp_f<0x4E>(rmin));
+  rmax = fmaxf(rmax, dpp_f<0x4E>(rmax));
+  rmin = fminf(rmin, dpp_f<0x141>(rmin));
+  rmax = fmaxf(rmax, dpp_f<0x141>(rmax));
+  rmin = fminf(rmin, dpp_f<0x140>(rmin));
+  rmax = fmaxf(rmax, dpp_f<0x140>(rmax));
   return dmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;
 }
 

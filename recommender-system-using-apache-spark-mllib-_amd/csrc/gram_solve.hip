@@ -1490,15 +1490,20 @@ __device__ __forceinline__ float diag_trace(const floatx4 (&A)[CN * (CN + 1) / 2
 // ratings).  Beyond kCondRankDef the row is re-solved in fp64.  tr_scaled: tr(G) in the
 // Gram's scale (x 1/inv2).
 constexpr float kCondRankDef = 64.f;
-__device__ __forceinline__ bool rank_deficient_illcond(float tr_scaled, float inv2, int64_t n, int k,
-                                                       float reg) {
-  return 4 * n <= (int64_t)k && tr_scaled * inv2 > (kCondRankDef - 1.f) * reg * (float)n;
+template <int CN>
+__device__ __forceinline__ bool rank_deficient_illcond(const floatx4 (&acc)[CN * (CN + 1) / 2],
+                                                       float inv2, int64_t n, int k, float reg) {
+  if (4 * n > (int64_t)k) return false;  // uniform: the trace only for very short rows
+  return diag_trace<CN>(acc, k) * inv2 > (kCondRankDef - 1.f) * reg * (float)n;
 }
 
 // Wave-uniform: do the scaled operands of a task with n terms miss the window?
+// (max over lanes < x <=> no lane at or above x: ballots, no reduction)
 __device__ __forceinline__ bool window_miss(float diag_lane, float n_terms, float rmax_lane) {
-  const float d = wave_max(diag_lane), r = wave_max(rmax_lane);
-  return (d > 0.f && d < n_terms * (kWindowT * kWindowT)) || (r > 0.f && r < kWindowT);
+  const bool dmiss = __ballot(diag_lane >= n_terms * (kWindowT * kWindowT)) == 0 &&
+                     __ballot(diag_lane > 0.f) != 0;
+  const bool rmiss = __ballot(rmax_lane >= kWindowT) == 0 && __ballot(rmax_lane > 0.f) != 0;
+  return dmiss || rmiss;
 }
 
 // Append `row` to the rescue list (one lane; each row is appended at most once per
@@ -1936,7 +1941,7 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
     rmax *= ldexpf(1.f, er);
     if (chunk < 0 && (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
-                      rank_deficient_illcond(diag_trace<CN>(acc, k), inv2, pe - pb, k, reg))) {
+                      rank_deficient_illcond<CN>(acc, inv2, pe - pb, k, reg))) {
       rescue_append(rescue_cnt, rescue_list, row);
       return;
     }
@@ -2036,7 +2041,7 @@ __global__ __launch_bounds__(64, ALS_PERSIST_OCC) void gram_solve_persist_kernel
         for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
       store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt, rmax);
     } else if (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
-               rank_deficient_illcond(diag_trace<CN>(acc, k), inv2, pe - pb, k, reg)) {
+               rank_deficient_illcond<CN>(acc, inv2, pe - pb, k, reg)) {
       rescue_append(rescue_cnt, rescue_list, row);
     } else {
       __syncthreads();  // staging area is reused by the solve
@@ -2318,7 +2323,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
     rmax *= ldexpf(1.f, er);
     if (chunk < 0 && (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
-                      rank_deficient_illcond(diag_trace<CN>(acc, k), inv2, pe - pb, k, reg))) {
+                      rank_deficient_illcond<CN>(acc, inv2, pe - pb, k, reg))) {
       rescue_append(rescue_cnt, rescue_list, row);
       return;
     }
@@ -3004,8 +3009,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
                                                     slot_bytes(k, n_chunks));
   unsigned* rescue_cnt = scal_u + 2;
-  if (phases & (ALS_PHASE_PREP | ALS_PHASE_RSCALE | ALS_PHASE_LAUNCH1))
-    ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));
+  // the rescue list starts empty at each Y prep (a fresh workspace holds garbage) and is
+  // emptied again after each RESCUE launch (row chunks of one half-sweep share one prep)
+  if (phases & ALS_PHASE_PREP) ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));
   const int cn = cn_for_k(k);
   const int kp = als_k_pad(k);
   const int zero_row = (int)n_src;

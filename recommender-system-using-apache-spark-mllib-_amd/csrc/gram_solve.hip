@@ -2532,50 +2532,84 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   }
 }
 
-// One wavefront per short light row (the tail of the longest-first light list: every
-// row with <= kDualMaxRatings ratings at k in (64, 128], KP = 128; <= kDualMaxRatings64
-// at k in (32, 64], KP = 64), explicit, regParam > 0.
-template <int KP>
-__global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
-    float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
-    const uint32_t* __restrict__ Ysp, int32_t zero_row, unsigned* __restrict__ rescue_cnt,
-    int32_t* __restrict__ rescue_list) {
-  static_assert(KP == 64 || KP == 128, "dual: k_pad 64 or 128");
-  constexpr int NMAX = KP == 128 ? kDualMaxRatings : kDualMaxRatings64;
-  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<KP == 128 ? 6 : 2>::SIZE];
+// The dual rows are the tail of the longest-first light list, so at KP = 128 the rows
+// of 65..96, 33..64 and <= 32 ratings are three consecutive ranges, solved by three
+// launches of their own block count NB (each with the registers of its own NB: one
+// kernel with a wave-uniform NB branch held NB = 6's 209 VGPRs for every row).  One
+// wave finds the two boundaries by a 64-way search (each step probes 64 evenly spaced
+// positions and ballots those still longer than the limit: 5 steps at 1e7 rows).
+// bounds[0] = first position with <= 64 ratings, bounds[1] = first with <= 32
+// (relative to the dual list).  A list out of order only costs speed: a row longer than
+// its class allows is re-solved by the fp64 rescue.
+__global__ __launch_bounds__(64) void dual_bounds_kernel(const int64_t* __restrict__ row_ptr,
+                                                         const int32_t* __restrict__ rows, int n,
+                                                         int32_t* __restrict__ bounds) {
   const int lane = threadIdx.x & 63;
-  const int row = rows[blockIdx.x];
-  const int64_t pb = row_ptr[row];
-  const int n = (int)(row_ptr[row + 1] - pb);
+#pragma unroll 1
+  for (int b = 0; b < 2; ++b) {
+    const int64_t lim = b == 0 ? 64 : 32;
+    int64_t lo = 0, hi = n;  // first position with <= lim ratings lies in [lo, hi]
+    while (hi > lo) {
+      const int64_t step = (hi - lo + 63) / 64;
+      const int64_t p = lo + lane * step;
+      bool longer = false;
+      if (p < hi) {
+        const int r = rows[p];
+        longer = row_ptr[r + 1] - row_ptr[r] > lim;
+      }
+      const int c = __popcll(__ballot(longer));
+      if (c == 0) {
+        hi = lo;
+      } else {
+        hi = min(hi, lo + c * step);
+        lo = lo + (c - 1) * step + 1;
+      }
+    }
+    if (lane == 0) bounds[b] = (int32_t)lo;
+  }
+}
+
+template <int NB>
+constexpr int dual_waves() { return NB == 6 ? 2 : (NB == 4 ? 3 : 5); }
+
+// Rows [b, e) of the dual list with <= 16 NB ratings, one wavefront per row, grid-stride
+// (the grid is sized to the class's resident waves).  KP = 64: every dual row (NB = 2,
+// e = n); KP = 128: the class NB of dual_bounds_kernel's ranges.  Explicit, reg > 0.
+template <int KP, int NB>
+__global__ __launch_bounds__(64, dual_waves<NB>()) void gram_solve_dual_kernel(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const int32_t* __restrict__ rows, int n_dual,
+    const int32_t* __restrict__ bounds, float* __restrict__ X, int ld, float reg,
+    int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
+    int32_t zero_row, unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
+  static_assert(KP == 64 || KP == 128, "dual: k_pad 64 or 128");
+  static_assert(KP == 128 ? (NB == 2 || NB == 4 || NB == 6) : NB == 2, "dual: NB per KP");
+  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<NB>::SIZE];
+  const int lane = threadIdx.x & 63;
+  const int b = (KP == 64 || NB == 6) ? 0 : bounds[NB == 4 ? 0 : 1];
+  const int e = (KP == 64 || NB == 2) ? n_dual : bounds[NB == 6 ? 0 : 1];
   const int ey = split_exponent(scal[0]);
-  float* xrow = X + (int64_t)row * ld;
-  if (n > NMAX) {  // schedule contract broken: report the row, leave it zero
-    if (lane == 0) atomicCAS(status, 0, row + 1);
-    return;
-  }
-  // ratings j = lane and j = lane + 64 (missing ones point at the zero row)
-  int cj[2];
-  float rj[2];
+#pragma unroll 1
+  for (int p = b + (int)blockIdx.x; p < e; p += (int)gridDim.x) {
+    const int row = rows[p];
+    const int64_t pb = row_ptr[row];
+    const int n = (int)(row_ptr[row + 1] - pb);
+    if (n > 16 * NB) {  // longer than the class (an unordered list): the fp64 solve
+      rescue_append(rescue_cnt, rescue_list, row);
+      continue;
+    }
+    // ratings j = lane and j = lane + 64 (missing ones point at the zero row)
+    int cj[2];
+    float rj[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int j = lane + 64 * h;
-    cj[h] = j < n ? col[pb + j] : zero_row;
-    rj[h] = j < n ? val[pb + j] : 0.f;
-  }
-  if constexpr (KP == 64) {
-    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt, rescue_list);
-  } else {
-    if (n <= 32)
-      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
-                       rescue_list);
-    else if (n <= 64)
-      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
-                       rescue_list);
-    else
-      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
-                       rescue_list);
+    for (int h = 0; h < 2; ++h) {
+      const int j = lane + 64 * h;
+      cj[h] = j < n ? col[pb + j] : zero_row;
+      rj[h] = j < n ? val[pb + j] : 0.f;
+    }
+    dual_row<NB, KP>(row, n, cj, rj, Ysp, ey, reg, X + (int64_t)row * ld, ld, lds, status,
+                     rescue_cnt, rescue_list);
+    wave_lds_sync();  // the next row reuses the LDS
   }
 }
 
@@ -2953,6 +2987,51 @@ static size_t slot_bytes(int32_t k, int32_t n_chunks) {
   return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
 }
 
+}  // extern "C"
+
+// The dual-path launches (gram_solve_dual_kernel): KP = 64 one class; KP = 128 the
+// class bounds, then NB = 6, 4, 2 over their ranges.  Grids: the class's resident
+// waves (256 CUs x 4 SIMDs x waves per SIMD), at most one block per dual row.
+template <int KP, int NB>
+static int dual_class_launch(const int64_t* row_ptr, const int32_t* col, const float* val,
+                              const int32_t* rows, int n_dual, const int32_t* bounds, float* X,
+                              int ld, float reg, int32_t* status, const float* scal,
+                              const uint32_t* Ysp, int32_t zero_row, unsigned* rescue_cnt,
+                              int32_t* rescue_list, hipStream_t st) {
+  const unsigned g = std::min<unsigned>((unsigned)n_dual, 256u * 4u * dual_waves<NB>());
+  gram_solve_dual_kernel<KP, NB><<<g, 64, 0, st>>>(row_ptr, col, val, rows, n_dual, bounds, X, ld,
+                                                   reg, status, scal, Ysp, zero_row, rescue_cnt,
+                                                   rescue_list);
+  ALS_LAUNCH_CHECK();
+  return ALS_OK;
+}
+
+template <int KP>
+static int dual_launch(const int64_t* row_ptr, const int32_t* col, const float* val,
+                        const int32_t* rows, int n_dual, int32_t* bounds, float* X, int ld,
+                        float reg, int32_t* status, const float* scal, const uint32_t* Ysp,
+                        int32_t zero_row, unsigned* rescue_cnt, int32_t* rescue_list,
+                        hipStream_t st) {
+  if constexpr (KP == 64) {
+    return dual_class_launch<64, 2>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
+                                    scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
+  } else {
+    dual_bounds_kernel<<<1, 64, 0, st>>>(row_ptr, rows, n_dual, bounds);
+    ALS_LAUNCH_CHECK();
+    int rc = dual_class_launch<128, 6>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
+                                       scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
+    if (rc == ALS_OK)
+      rc = dual_class_launch<128, 4>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
+                                     scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
+    if (rc == ALS_OK)
+      rc = dual_class_launch<128, 2>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
+                                     scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
+    return rc;
+  }
+}
+
+extern "C" {
+
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows) {
   // 256 B of scale words (max |Y_src|, max |rating|, rescue count) | split table
   // ((n_src + 1) x k_pad words, explicit) | partial slots of the heavy-row chunks |
@@ -3049,6 +3128,15 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const unsigned gd = (phases & ALS_PHASE_DUAL) ? (unsigned)(n_light - n_light_primal) : 0u;
   const unsigned g2 = (phases & ALS_PHASE_LAUNCH2) ? (unsigned)n_heavy : 0u;
   const bool rescue = (phases & ALS_PHASE_RESCUE) && n_rows > 0;
+  int32_t* dual_bounds = reinterpret_cast<int32_t*>(scal_u + 4);
+#define ALS_RC(expr)                   \
+  do {                                 \
+    const int rc_ = (expr);            \
+    if (rc_ != ALS_OK) return rc_;     \
+  } while (0)
+#define DUAL_ARGS                                                                                 \
+  row_ptr, col, val, light_rows + n_light_primal, (int)gd, dual_bounds, X_dst, ld, reg, status_dev, \
+      scal, Ysp, zero_row, rescue_cnt, rescue_list, st
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
     if (g1 && ALS_PERSIST && !IMP)                                                                \
@@ -3062,13 +3150,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                     alpha, yty_packed, slots, status_dev, scal,   \
                                                     Ysp, kp, zero_row, rescue_cnt, rescue_list);  \
     ALS_LAUNCH_CHECK();                                                                           \
-    if (gd && CN == 4 && !IMP) {                                                                  \
-      gram_solve_dual_kernel<64><<<gd, 64, 0, st>>>(row_ptr, col, val,                            \
-                                                    light_rows + n_light_primal, X_dst, ld, reg,  \
-                                                    status_dev, scal, Ysp, zero_row, rescue_cnt,  \
-                                                    rescue_list);                                 \
-      ALS_LAUNCH_CHECK();                                                                         \
-    }                                                                                             \
+    if (gd && CN == 4 && !IMP) ALS_RC(dual_launch<64>(DUAL_ARGS));                                        \
     if (g2) {                                                                                     \
       heavy_sum_f64_kernel<Cfg<CN>::SLOT, IMP>                                                    \
           <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots);       \
@@ -3096,13 +3178,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                    status_dev, scal, Ysp, kp, zero_row,           \
                                                    rescue_cnt, rescue_list);                      \
     ALS_LAUNCH_CHECK();                                                                           \
-    if (gd) {                                                                                     \
-      gram_solve_dual_kernel<128><<<gd, 64, 0, st>>>(row_ptr, col, val,                           \
-                                                     light_rows + n_light_primal, X_dst, ld, reg, \
-                                                     status_dev, scal, Ysp, zero_row, rescue_cnt, \
-                                                     rescue_list);                                \
-      ALS_LAUNCH_CHECK();                                                                         \
-    }                                                                                             \
+    if (gd) ALS_RC(dual_launch<128>(DUAL_ARGS));                                                          \
     if (g2) {                                                                                     \
       heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot + 255) / 256, g2), 256, 0, st>>>(                 \
           heavy_slot_begin, slots_f, yty_packed);                                                 \
@@ -3133,6 +3209,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   }
 #undef ALS_SOLVE_W1_LAUNCH
 #undef ALS_SOLVE_LAUNCH
+#undef DUAL_ARGS
+#undef ALS_RC
   return ALS_OK;
 }
 

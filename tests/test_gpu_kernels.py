@@ -9,6 +9,7 @@ Bars (DESIGN.md "Parity"):
     RMSE within 1e-9; computeError KAT (output.txt:16-18) exact to 11 digits.
   * K5 (top-k): identical indices except where the oracle's fp64 scores tie within 1e-5.
 """
+import dataclasses
 import json
 import math
 import os
@@ -302,6 +303,39 @@ def test_dual_short_rows_match_primal_and_oracle(rank, reg):
                      for a, b in ((0, 16), (16, 32), (32, 64), (64, 10 ** 9))}
         assert e.max() <= 1e-4, (dual, out[dual])
     report(f"dual_vs_primal[rank={rank},reg={reg:g}]", out)
+
+
+def test_dual_classes_from_an_unordered_list():
+    """At rank 65-128 the dual rows are solved in three launches (65-96, 33-64 and <= 32
+    ratings, NB = 6 / 4 / 2) over ranges found on the device by searching the
+    longest-first light list.  The light list reversed and shuffled breaks that order:
+    a row longer than its class allows must then go to the fp64 rescue, a shorter one
+    is padded — never a wrong or missing row."""
+    rank, reg = 128, 0.1
+    degrees = DUAL_DEGREES * 20
+    u, i, r = _degree_data(degrees, 400, seed=11)
+    core = _core(u, i, r, chunk=256)
+    ub = core.user_block
+    core.init_factors(rank, seed=3)
+    V0 = core.V[:, :rank].cpu().numpy()
+    U_ref = O.half_sweep(ub.row_ptr.cpu().numpy(), ub.col.cpu().numpy(), ub.val.cpu().numpy(),
+                         V0, reg)
+    nd = ub.n_dual(rank)
+    n_primal = ub.n_light - nd
+    g = torch.Generator(device="cpu")
+    g.manual_seed(5)
+    for order in ("reversed", "shuffled"):
+        tail = ub.light_rows[n_primal:ub.n_light].clone()
+        tail = tail.flip(0) if order == "reversed" else tail[torch.randperm(nd, generator=g).to(DEV)]
+        blk = dataclasses.replace(ub, light_rows=torch.cat([ub.light_rows[:n_primal], tail]))
+        core.U.fill_(7.0)
+        core.status.zero_()
+        E.solve_half(blk, core.V, core.U, rank, reg, False, 1.0, None, core.status, core.ws)
+        torch.cuda.synchronize()
+        core.check_status()
+        e = rel_row_errs(core.U[:, :rank].cpu().numpy(), U_ref)
+        report(f"dual_unordered[{order}]", {"max_rel": float(e.max())})
+        assert e.max() <= 1e-4, (order, float(e.max()))
 
 
 def _exact_rel_errs(x, ref):

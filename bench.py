@@ -461,19 +461,8 @@ def _n_dual(block, k: int, imp: bool, reg: float = 0.1) -> int:
     return 0 if (imp or reg <= 0) else block.n_dual(k)
 
 
-DUAL_WAVES = {6: 2, 4: 3, 2: 5}  # csrc/gram_solve.hip dual_waves<NB>: resident waves per SIMD
-
-
-def dual_parts(n_dual: int, k: int):
-    """The dual launches of a half-sweep (ALS_PHASE_DUAL): [(kernel, grid threads)] —
-    k <= 64 one class (NB = 2); k > 64 the classes of 65-96, 33-64 and <= 32 ratings
-    (NB = 6, 4, 2), each a grid-stride launch of min(n_dual, 1024 x its waves per SIMD)
-    one-wave blocks (csrc/gram_solve.hip dual_class_launch)."""
-    if n_dual <= 0:
-        return []
-    kp, nbs = (128, (6, 4, 2)) if k > 64 else (64, (2,))
-    return [(f"gram_solve_dual_kernel<{kp}, {nb}>", 64 * min(n_dual, 1024 * DUAL_WAVES[nb]))
-            for nb in nbs]
+def dual_kernel(k: int) -> str:
+    return f"gram_solve_dual_kernel<{128 if k > 64 else 64}>"
 
 
 def _launch1_parts(block, k: int, imp: bool, reg: float = 0.1):
@@ -483,14 +472,16 @@ def _launch1_parts(block, k: int, imp: bool, reg: float = 0.1):
     kern = dominant_kernel(k, imp)
     n_dual = _n_dual(block, k, imp, reg)
     parts = [(kern, 64 * (block.n_chunks + block.n_light - n_dual))]
-    return parts + dual_parts(n_dual, k)
+    if n_dual > 0:
+        parts.append((dual_kernel(k), 64 * n_dual))
+    return parts
 
 
 def dual_view(workload: str, k: int, blocks: dict, ms: dict, reg: float):
     """The dual launch of each half-sweep (explicit short rows): event time, algorithmic
     bytes (each rating's factor row + index + rating, each row's output) and HBM
     fraction, plus that kernel's PMC view when profiled."""
-    out = {"kernels": [kn for kn, _ in dual_parts(1, k)], "launches": {}}
+    out = {"kernel": dual_kernel(k), "launches": {}}
     for name, blk in blocks.items():
         nd = _n_dual(blk, k, False, reg)
         if nd == 0:
@@ -499,7 +490,7 @@ def dual_view(workload: str, k: int, blocks: dict, ms: dict, reg: float):
         t = ms[name] * 1e-3
         ent = {"rows": nd, "nnz": blk.dual_nnz(k), "event_ms": ms[name], "algorithmic_bytes": b,
                "hbm_frac": b / t / 1e9 / PEAK_HBM_GBS}
-        pv = _pmc_view(_combine_pmc(workload, dual_parts(nd, k)), t)
+        pv = _pmc_view(load_pmc(workload, dual_kernel(k), 64 * nd), t)
         if pv:
             ent["pmc"] = pv
         out["launches"][name] = ent

@@ -57,13 +57,6 @@ constexpr int kRescueGrid = 256;     // workgroups walking the rescue list (resc
 // the diagonal stays within a few times lambda n); implicit confidences spanning six
 // decades spread by 1e3-1e5 and reach 1e-3 errors in fp32.
 constexpr float kCondMax = 32.f;
-#ifndef ALS_PERSIST
-#define ALS_PERSIST 0
-#endif
-#ifndef ALS_PERSIST_OCC
-#define ALS_PERSIST_OCC 3
-#endif
-constexpr int kPersistWaves = 256 * 4 * 3 * 2;  // CUs x SIMDs x waves/SIMD x 2
 constexpr int kMaxRank = 128;
 
 template <int CN>
@@ -1284,77 +1277,6 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& dse
   return dmin;
 }
 
-// x of row group G broadcast to all four row groups (two VALU lane swaps:
-// v_permlane32_swap gives rows {0,1} (or {2,3}) in both halves, v_permlane16_swap then
-// row 2h (or 2h+1) in all four).
-template <int G>
-__device__ __forceinline__ float rowgroup_bcast(float x) {
-  uint32_t a = __builtin_bit_cast(uint32_t, x), b = a;
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
-  uint32_t c = G < 2 ? a : b, d = c;
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
-  return __builtin_bit_cast(float, (G & 1) ? d : c);
-}
-
-// v on the lanes of 64-bit mask M (a constant), else w.
-template <uint64_t M>
-__device__ __forceinline__ float sel_mask(float v, float w) {
-  float r;
-  asm volatile("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(v), "v"(w), "s"(M));
-  return r;
-}
-
-// The sweep of sweep16 on a symmetric 16 x 16 block held in the MFMA C layout (lane
-// (q, m): B[4q + r][m], r = 0..3) instead of column per lane: per pivot p, row p is
-// broadcast from row group p/4 to all four (rowgroup_bcast), and a lane's four column-p
-// entries come from lane p of its own row group (v_fmac_f32_dpp row_newbcast:p), so a
-// lane updates its four entries, not sixteen replicated ones, and the block never goes
-// through LDS (the result is already in the C layout the Pm / Schur MFMAs read).  Every
-// entry sees the same fp32 operations, in the same order, as in sweep16 (deferred
-// pivot-column scaling, look-ahead of the next pivot).
-template <class Hook>
-__device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
-  float B[4] = {Bv[0], Bv[1], Bv[2], Bv[3]};
-  float dmin = 3.0e38f;
-  float dself = 1.f;
-  float rowp = rowgroup_bcast<0>(B[0]);
-  float d = bcast16<0>(rowp);
-  float rd = rcp_t(d);
-  float f = rowp * rd;
-  float nf = sel_lane16<0>(0.f, -f);
-  static_for<16>([&](auto pc) {
-    constexpr int p = decltype(pc)::value;
-    constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
-    dmin = fminf(dmin, d);
-    asm volatile("s_nop 1" ::: "memory");
-    // the register holding row p+1 first: then pivot p+1's row is final
-    fmac_bcast16<p>(B[rn], nf);
-    float dn = 0.f, rdn = 0.f, fn = 0.f, nfn = 0.f;
-    if constexpr (p + 1 < 16) {
-      constexpr int qn = (p + 1) >> 2;
-      const float rown = rowgroup_bcast<qn>(B[rn]);
-      dn = bcast16<p + 1>(rown);
-      rdn = rcp_t(dn);
-      fn = rown * rdn;
-      nfn = sel_lane16<p + 1>(0.f, -fn);
-    }
-    static_for<4>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if constexpr (r != rn) fmac_bcast16<p>(B[r], nf);
-    });
-    // row p (row group qp): f off the pivot, -1 on it (scaled by 1/d at the end)
-    B[rp] = sel_mask<0xFFFFull << (16 * qp)>(sel_lane16<p>(-1.f, f), B[rp]);
-    dself = sel_lane16<p>(d, dself);
-    hook(pc);
-    d = dn; rd = rdn; f = fn; nf = nfn;
-  });
-  const float s = rcp_t(dself);
-#pragma unroll
-  for (int r = 0; r < 4; ++r) Bv[r] = B[r] * s;
-  dself_out = dself;
-  return dmin;
-}
-
 // Schur tiles of step K, I-major: u = 0 is (K+1, K+1), the next pivot block.
 template <int NB>
 __host__ __device__ constexpr int schur_n(int K) { return (NB - 1 - K) * (NB - K) / 2; }
@@ -1393,21 +1315,9 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 // 8.1 ms/iter measured).
 template <int NB>
 constexpr bool kW1SplitSchur = NB == 8;
-// Split-f16 Schur / Pm products in the explicit light-row solves (A/B under test):
-// the k <= 64 W1<4> solve, the rank-65-128 W1 light rows and the n x n dual systems.
-#ifndef ALS_K64_SPLIT
-#define ALS_K64_SPLIT 0
-#endif
-// W1-family solves sweep their diagonal blocks in the MFMA C layout (sweep16c)
-#ifndef ALS_SWEEP_C
-#define ALS_SWEEP_C 0
-#endif
-#ifndef ALS_W1E_SPLIT
-#define ALS_W1E_SPLIT 0
-#endif
-#ifndef ALS_DUAL_SPLIT
-#define ALS_DUAL_SPLIT 0
-#endif
+// Measured round 4 (A/B at configs[1] / configs[3]): the split form in the explicit
+// k <= 64 solve (2.33 vs 2.26 ms/iter), the explicit rank-128 light rows (user launch
+// 112 vs 102 ms) and the n x n dual systems (76 vs 70 ms) is slower: fp32 stays there.
 
 // fp32 form: acc += X^T Y (the MFMA's k index is permuted to 4q + s4).
 __device__ __forceinline__ floatx4 tile_xty(const floatx4& X, const floatx4& Y, floatx4 acc) {
@@ -1588,43 +1498,30 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   floatx4 Gm, bk;
   auto pivot_block = [&](auto Kc, auto&& hook) {
     constexpr int K = decltype(Kc)::value;
-    if constexpr (ALS_SWEEP_C) {
-      // swept in the C layout: Gm comes out where the MFMAs read it
-      Gm = A[w1_tile<NB>(K, K)];
-      float ds;
-      dmin = fminf(dmin, sweep16c(Gm, hook, ds));
-      track_pivot(ds, m * NB + K < k);
-      const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
-      if (q == 0) vec[m] = bK;
-      wave_lds_order();
-      bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);  // row layout
-      wave_lds_order();
-    } else {
-      *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile<NB>(K, K)];
-      wave_lds_order();
-      float R[16];
+    *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile<NB>(K, K)];
+    wave_lds_order();
+    float R[16];
 #pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * c4);
-        R[4 * c4] = v[0]; R[4 * c4 + 1] = v[1]; R[4 * c4 + 2] = v[2]; R[4 * c4 + 3] = v[3];
-      }
-      float ds;
-      dmin = fminf(dmin, sweep16(R, hook, ds));
-      track_pivot(ds, m * NB + K < k);
-      wave_lds_order();
-      const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
-      if (q == 0) {
-#pragma unroll
-        for (int c4 = 0; c4 < 4; ++c4)
-          *reinterpret_cast<floatx4*>(col + m * CS + 4 * c4) =
-              floatx4{R[4 * c4], R[4 * c4 + 1], R[4 * c4 + 2], R[4 * c4 + 3]};
-        vec[m] = bK;
-      }
-      wave_lds_order();
-      Gm = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * q);  // C layout
-      bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);           // row layout
-      wave_lds_order();
+    for (int c4 = 0; c4 < 4; ++c4) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * c4);
+      R[4 * c4] = v[0]; R[4 * c4 + 1] = v[1]; R[4 * c4 + 2] = v[2]; R[4 * c4 + 3] = v[3];
     }
+    float ds;
+    dmin = fminf(dmin, sweep16(R, hook, ds));
+    track_pivot(ds, m * NB + K < k);
+    wave_lds_order();
+    const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
+    if (q == 0) {
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4)
+        *reinterpret_cast<floatx4*>(col + m * CS + 4 * c4) =
+            floatx4{R[4 * c4], R[4 * c4 + 1], R[4 * c4 + 2], R[4 * c4 + 3]};
+      vec[m] = bK;
+    }
+    wave_lds_order();
+    Gm = *reinterpret_cast<const floatx4*>(col + m * CS + 4 * q);  // C layout
+    bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);           // row layout
+    wave_lds_order();
   };
   // step-K operands of the split form: block row K ([hi|lo] of sK A_KJ), Pm halves
   half8v XK[NB], Ph[NB], Pl[NB];
@@ -1963,109 +1860,11 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     // rank 33-64 explicit: the W1 block elimination on 4 x 4 tiles (swept diagonal
     // inverses + fp32 MFMA), in the Gram's scale
     static_assert(W1LdsT<4>::SIZE <= PanelLds<4>::SIZE, "W1<4> LDS");
-    w1_finish_and_solve<false, 4, (bool)ALS_K64_SPLIT>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
+    w1_finish_and_solve<false, 4, false>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
                                   X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
   } else {
     finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty,
                                           X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
-  }
-}
-
-// Persistent form of gram_solve_kernel for explicit feedback at k <= 64 (A/B under
-// test, ALS_PERSIST): a grid of resident waves walks the launch-1 task list with a
-// stride (task order is the LPT order, so every wave still meets long rows first),
-// and the next task's schedule entries (light_rows -> row_ptr, or the chunk bounds)
-// are loaded while the current task runs, so the chain of dependent loads that starts
-// every one-task wave is off the critical path.  Same arithmetic as gram_solve_kernel.
-template <int CN>
-__global__ __launch_bounds__(64, ALS_PERSIST_OCC) void gram_solve_persist_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, const int32_t* __restrict__ light_rows,
-    const int64_t* __restrict__ chunk_begin, const int64_t* __restrict__ chunk_end,
-    int32_t n_chunks, int32_t n_light, float* __restrict__ X, int ld, int k, float reg,
-    double* __restrict__ slots, int32_t* __restrict__ status, const float* __restrict__ scal,
-    const uint32_t* __restrict__ Ysp, int32_t kp, int32_t zero_row,
-    unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
-  constexpr int NT = Cfg<CN>::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
-  const int n_tasks = n_chunks + n_light;
-  int t = blockIdx.x;
-  if (t >= n_tasks) return;
-  const int ey = split_exponent(scal[0]), er = split_exponent(scal[1]);
-  const float inv2 = ldexpf(1.f, -2 * ey);
-  int chunk, light;
-  decode_task(t, n_chunks, n_light, chunk, light);
-  int row = chunk >= 0 ? -1 : light_rows[light];
-  int64_t pb = chunk >= 0 ? chunk_begin[chunk] : row_ptr[row];
-  int64_t pe = chunk >= 0 ? chunk_end[chunk] : row_ptr[row + 1];
-  for (;;) {
-    // the next task's first schedule load, in flight during this task's Gram
-    const int tn = t + (int)gridDim.x;
-    const bool more = tn < n_tasks;
-    int nchunk = -1, nlight = -1, nrow = -1;
-    int64_t npb = 0, npe = 0;
-    if (more) {
-      decode_task(tn, n_chunks, n_light, nchunk, nlight);
-      if (nchunk >= 0) {
-        npb = chunk_begin[nchunk];
-        npe = chunk_end[nchunk];
-      } else {
-        nrow = light_rows[nlight];
-      }
-    }
-    floatx4 acc[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-    float bt[CN];
-    float rmax = 0.f;
-    {
-      floatx4 accb[CN];
-#pragma unroll
-      for (int c = 0; c < CN; ++c) accb[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-      gram_accumulate_pre<FullTiles<CN>>(col, val, pb, pe, Ysp, (uint32_t)kp, zero_row,
-                                         ldexpf(1.f, er), (threadIdx.x & 15) * CN, acc, accb,
-                                         reinterpret_cast<int*>(smem), rmax);
-      rhs_from_tiles<FullTiles<CN>>(accb, ldexpf(1.f, -ey - er), bt);
-    }
-    // the next row's bounds, in flight during this task's solve
-    if (more && nchunk < 0) {
-      npb = row_ptr[nrow];
-      npe = row_ptr[nrow + 1];
-    }
-    rmax *= ldexpf(1.f, er);
-    if (chunk >= 0) {
-      float tot[NT][4];
-#pragma unroll
-      for (int i = 0; i < NT; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
-      store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt, rmax);
-    } else if (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
-               rank_deficient_illcond<CN>(acc, inv2, pe - pb, k, reg)) {
-      rescue_append(rescue_cnt, rescue_list, row);
-    } else {
-      __syncthreads();  // staging area is reused by the solve
-      if constexpr (CN == 4) {
-        w1_finish_and_solve<false, 4, (bool)ALS_K64_SPLIT>(acc, inv2, bt, pe - pb, nullptr, smem, k,
-                                                           reg, X + (int64_t)row * ld, ld, row,
-                                                           rescue_cnt, rescue_list);
-      } else {
-        float tot[NT][4];
-#pragma unroll
-        for (int i = 0; i < NT; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) tot[i][r] = acc[i][r] * inv2;
-        finish_and_solve<CN, false, float>(tot, bt, pe - pb, smem, k, reg, nullptr,
-                                           X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
-      }
-    }
-    if (!more) break;
-    __syncthreads();  // the solve's LDS is reused by the next Gram's staging
-    t = tn;
-    chunk = nchunk;
-    row = nrow;
-    pb = npb;
-    pe = npe;
   }
 }
 
@@ -2342,7 +2141,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT || (bool)ALS_W1E_SPLIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
+  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
                                                X + (int64_t)row * ld, ld, row, rescue_cnt,
                                                rescue_list);
 }
@@ -2476,7 +2275,7 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   float bcol[NB], z[NB];
 #pragma unroll
   for (int c = 0; c < NB; ++c) bcol[c] = rc[c] * inv;
-  const bool ok = w1_solve_x<NB, (bool)ALS_DUAL_SPLIT>(acc, bcol, lds, n, z);
+  const bool ok = w1_solve_x<NB, false>(acc, bcol, lds, n, z);
   if (!ok) {  // re-solved in fp64 (the primal k x k system)
     rescue_append(rescue_cnt, rescue_list, row);
     return;
@@ -2532,84 +2331,50 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   }
 }
 
-// The dual rows are the tail of the longest-first light list, so at KP = 128 the rows
-// of 65..96, 33..64 and <= 32 ratings are three consecutive ranges, solved by three
-// launches of their own block count NB (each with the registers of its own NB: one
-// kernel with a wave-uniform NB branch held NB = 6's 209 VGPRs for every row).  One
-// wave finds the two boundaries by a 64-way search (each step probes 64 evenly spaced
-// positions and ballots those still longer than the limit: 5 steps at 1e7 rows).
-// bounds[0] = first position with <= 64 ratings, bounds[1] = first with <= 32
-// (relative to the dual list).  A list out of order only costs speed: a row longer than
-// its class allows is re-solved by the fp64 rescue.
-__global__ __launch_bounds__(64) void dual_bounds_kernel(const int64_t* __restrict__ row_ptr,
-                                                         const int32_t* __restrict__ rows, int n,
-                                                         int32_t* __restrict__ bounds) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll 1
-  for (int b = 0; b < 2; ++b) {
-    const int64_t lim = b == 0 ? 64 : 32;
-    int64_t lo = 0, hi = n;  // first position with <= lim ratings lies in [lo, hi]
-    while (hi > lo) {
-      const int64_t step = (hi - lo + 63) / 64;
-      const int64_t p = lo + lane * step;
-      bool longer = false;
-      if (p < hi) {
-        const int r = rows[p];
-        longer = row_ptr[r + 1] - row_ptr[r] > lim;
-      }
-      const int c = __popcll(__ballot(longer));
-      if (c == 0) {
-        hi = lo;
-      } else {
-        hi = min(hi, lo + c * step);
-        lo = lo + (c - 1) * step + 1;
-      }
-    }
-    if (lane == 0) bounds[b] = (int32_t)lo;
-  }
-}
-
-template <int NB>
-constexpr int dual_waves() { return NB == 6 ? 2 : (NB == 4 ? 3 : 5); }
-
-// Rows [b, e) of the dual list with <= 16 NB ratings, one wavefront per row, grid-stride
-// (the grid is sized to the class's resident waves).  KP = 64: every dual row (NB = 2,
-// e = n); KP = 128: the class NB of dual_bounds_kernel's ranges.  Explicit, reg > 0.
-template <int KP, int NB>
-__global__ __launch_bounds__(64, dual_waves<NB>()) void gram_solve_dual_kernel(
+// One wavefront per short light row (the tail of the longest-first light list: every
+// row with <= kDualMaxRatings ratings at k in (64, 128], KP = 128; <= kDualMaxRatings64
+// at k in (32, 64], KP = 64), explicit, regParam > 0.
+template <int KP>
+__global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
-    const float* __restrict__ val, const int32_t* __restrict__ rows, int n_dual,
-    const int32_t* __restrict__ bounds, float* __restrict__ X, int ld, float reg,
-    int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
-    int32_t zero_row, unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
+    const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
+    float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
+    const uint32_t* __restrict__ Ysp, int32_t zero_row, unsigned* __restrict__ rescue_cnt,
+    int32_t* __restrict__ rescue_list) {
   static_assert(KP == 64 || KP == 128, "dual: k_pad 64 or 128");
-  static_assert(KP == 128 ? (NB == 2 || NB == 4 || NB == 6) : NB == 2, "dual: NB per KP");
-  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<NB>::SIZE];
+  constexpr int NMAX = KP == 128 ? kDualMaxRatings : kDualMaxRatings64;
+  __shared__ __attribute__((aligned(16))) float lds[W1LdsT<KP == 128 ? 6 : 2>::SIZE];
   const int lane = threadIdx.x & 63;
-  const int b = (KP == 64 || NB == 6) ? 0 : bounds[NB == 4 ? 0 : 1];
-  const int e = (KP == 64 || NB == 2) ? n_dual : bounds[NB == 6 ? 0 : 1];
+  const int row = rows[blockIdx.x];
+  const int64_t pb = row_ptr[row];
+  const int n = (int)(row_ptr[row + 1] - pb);
   const int ey = split_exponent(scal[0]);
-#pragma unroll 1
-  for (int p = b + (int)blockIdx.x; p < e; p += (int)gridDim.x) {
-    const int row = rows[p];
-    const int64_t pb = row_ptr[row];
-    const int n = (int)(row_ptr[row + 1] - pb);
-    if (n > 16 * NB) {  // longer than the class (an unordered list): the fp64 solve
-      rescue_append(rescue_cnt, rescue_list, row);
-      continue;
-    }
-    // ratings j = lane and j = lane + 64 (missing ones point at the zero row)
-    int cj[2];
-    float rj[2];
+  float* xrow = X + (int64_t)row * ld;
+  if (n > NMAX) {  // schedule contract broken: report the row, leave it zero
+    if (lane == 0) atomicCAS(status, 0, row + 1);
+    return;
+  }
+  // ratings j = lane and j = lane + 64 (missing ones point at the zero row)
+  int cj[2];
+  float rj[2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = lane + 64 * h;
-      cj[h] = j < n ? col[pb + j] : zero_row;
-      rj[h] = j < n ? val[pb + j] : 0.f;
-    }
-    dual_row<NB, KP>(row, n, cj, rj, Ysp, ey, reg, X + (int64_t)row * ld, ld, lds, status,
-                     rescue_cnt, rescue_list);
-    wave_lds_sync();  // the next row reuses the LDS
+  for (int h = 0; h < 2; ++h) {
+    const int j = lane + 64 * h;
+    cj[h] = j < n ? col[pb + j] : zero_row;
+    rj[h] = j < n ? val[pb + j] : 0.f;
+  }
+  if constexpr (KP == 64) {
+    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt, rescue_list);
+  } else {
+    if (n <= 32)
+      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
+                       rescue_list);
+    else if (n <= 64)
+      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
+                       rescue_list);
+    else
+      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
+                       rescue_list);
   }
 }
 
@@ -2987,51 +2752,6 @@ static size_t slot_bytes(int32_t k, int32_t n_chunks) {
   return align_up(sizeof(double) * slot_doubles(k) * (size_t)(n_chunks > 0 ? n_chunks : 0));
 }
 
-}  // extern "C"
-
-// The dual-path launches (gram_solve_dual_kernel): KP = 64 one class; KP = 128 the
-// class bounds, then NB = 6, 4, 2 over their ranges.  Grids: the class's resident
-// waves (256 CUs x 4 SIMDs x waves per SIMD), at most one block per dual row.
-template <int KP, int NB>
-static int dual_class_launch(const int64_t* row_ptr, const int32_t* col, const float* val,
-                              const int32_t* rows, int n_dual, const int32_t* bounds, float* X,
-                              int ld, float reg, int32_t* status, const float* scal,
-                              const uint32_t* Ysp, int32_t zero_row, unsigned* rescue_cnt,
-                              int32_t* rescue_list, hipStream_t st) {
-  const unsigned g = std::min<unsigned>((unsigned)n_dual, 256u * 4u * dual_waves<NB>());
-  gram_solve_dual_kernel<KP, NB><<<g, 64, 0, st>>>(row_ptr, col, val, rows, n_dual, bounds, X, ld,
-                                                   reg, status, scal, Ysp, zero_row, rescue_cnt,
-                                                   rescue_list);
-  ALS_LAUNCH_CHECK();
-  return ALS_OK;
-}
-
-template <int KP>
-static int dual_launch(const int64_t* row_ptr, const int32_t* col, const float* val,
-                        const int32_t* rows, int n_dual, int32_t* bounds, float* X, int ld,
-                        float reg, int32_t* status, const float* scal, const uint32_t* Ysp,
-                        int32_t zero_row, unsigned* rescue_cnt, int32_t* rescue_list,
-                        hipStream_t st) {
-  if constexpr (KP == 64) {
-    return dual_class_launch<64, 2>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
-                                    scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
-  } else {
-    dual_bounds_kernel<<<1, 64, 0, st>>>(row_ptr, rows, n_dual, bounds);
-    ALS_LAUNCH_CHECK();
-    int rc = dual_class_launch<128, 6>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
-                                       scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
-    if (rc == ALS_OK)
-      rc = dual_class_launch<128, 4>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
-                                     scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
-    if (rc == ALS_OK)
-      rc = dual_class_launch<128, 2>(row_ptr, col, val, rows, n_dual, bounds, X, ld, reg, status,
-                                     scal, Ysp, zero_row, rescue_cnt, rescue_list, st);
-    return rc;
-  }
-}
-
-extern "C" {
-
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows) {
   // 256 B of scale words (max |Y_src|, max |rating|, rescue count) | split table
   // ((n_src + 1) x k_pad words, explicit) | partial slots of the heavy-row chunks |
@@ -3128,29 +2848,22 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const unsigned gd = (phases & ALS_PHASE_DUAL) ? (unsigned)(n_light - n_light_primal) : 0u;
   const unsigned g2 = (phases & ALS_PHASE_LAUNCH2) ? (unsigned)n_heavy : 0u;
   const bool rescue = (phases & ALS_PHASE_RESCUE) && n_rows > 0;
-  int32_t* dual_bounds = reinterpret_cast<int32_t*>(scal_u + 4);
-#define ALS_RC(expr)                   \
-  do {                                 \
-    const int rc_ = (expr);            \
-    if (rc_ != ALS_OK) return rc_;     \
-  } while (0)
-#define DUAL_ARGS                                                                                 \
-  row_ptr, col, val, light_rows + n_light_primal, (int)gd, dual_bounds, X_dst, ld, reg, status_dev, \
-      scal, Ysp, zero_row, rescue_cnt, rescue_list, st
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
-    if (g1 && ALS_PERSIST && !IMP)                                                                \
-      gram_solve_persist_kernel<CN><<<std::min<unsigned>(g1, kPersistWaves), 64, 0, st>>>(        \
-          row_ptr, col, val, light_rows, chunk_begin, chunk_end, n_chunks, n_light_primal, X_dst, \
-          ld, k, reg, slots, status_dev, scal, Ysp, kp, zero_row, rescue_cnt, rescue_list);       \
-    else if (g1)                                                                                  \
+    if (g1)                                                                                       \
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
                                                     chunk_begin, chunk_end, n_chunks,             \
                                                     n_light_primal, Y_src, X_dst, ld, k, reg,     \
                                                     alpha, yty_packed, slots, status_dev, scal,   \
                                                     Ysp, kp, zero_row, rescue_cnt, rescue_list);  \
     ALS_LAUNCH_CHECK();                                                                           \
-    if (gd && CN == 4 && !IMP) ALS_RC(dual_launch<64>(DUAL_ARGS));                                        \
+    if (gd && CN == 4 && !IMP) {                                                                  \
+      gram_solve_dual_kernel<64><<<gd, 64, 0, st>>>(row_ptr, col, val,                            \
+                                                    light_rows + n_light_primal, X_dst, ld, reg,  \
+                                                    status_dev, scal, Ysp, zero_row, rescue_cnt,  \
+                                                    rescue_list);                                 \
+      ALS_LAUNCH_CHECK();                                                                         \
+    }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_f64_kernel<Cfg<CN>::SLOT, IMP>                                                    \
           <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots);       \
@@ -3178,7 +2891,13 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                    status_dev, scal, Ysp, kp, zero_row,           \
                                                    rescue_cnt, rescue_list);                      \
     ALS_LAUNCH_CHECK();                                                                           \
-    if (gd) ALS_RC(dual_launch<128>(DUAL_ARGS));                                                          \
+    if (gd) {                                                                                     \
+      gram_solve_dual_kernel<128><<<gd, 64, 0, st>>>(row_ptr, col, val,                           \
+                                                     light_rows + n_light_primal, X_dst, ld, reg, \
+                                                     status_dev, scal, Ysp, zero_row, rescue_cnt, \
+                                                     rescue_list);                                \
+      ALS_LAUNCH_CHECK();                                                                         \
+    }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot + 255) / 256, g2), 256, 0, st>>>(                 \
           heavy_slot_begin, slots_f, yty_packed);                                                 \
@@ -3209,8 +2928,6 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   }
 #undef ALS_SOLVE_W1_LAUNCH
 #undef ALS_SOLVE_LAUNCH
-#undef DUAL_ARGS
-#undef ALS_RC
   return ALS_OK;
 }
 

@@ -4,7 +4,7 @@
 # by tools/ab_solve.py).  Usage: bash tools/ab/build_solve.sh tag='-DX=1 -DY=0' ...
 set -e
 cd "$(dirname "$0")"
-CSRC=../../recommender-system-using-apache-spark-mllib-_amd/csrc
+CSRC=${CSRC:-../../recommender-system-using-apache-spark-mllib-_amd/csrc}
 for a in "$@"; do
   t=${a%%=*}; f=${a#*=}
   mkdir -p obj_$t

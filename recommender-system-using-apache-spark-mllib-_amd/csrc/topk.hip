@@ -78,9 +78,6 @@ __global__ __launch_bounds__(256) void tk_absmax_kernel(const float* __restrict_
 }  // namespace
 
 constexpr int kTopkMax = 256;
-#ifndef ALS_TK_BPREF
-#define ALS_TK_BPREF 0
-#endif
 constexpr int kLdsBytes = 160 * 1024;  // per CU on gfx950 (one workgroup may use it all)
 
 // Lists hold (score, index) as one 64-bit key whose unsigned order is the
@@ -492,15 +489,11 @@ __device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
 // stream (the first tiles re-staged: compute / LDS only).
 // Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
 // rows), 4 with LDS lists (top > 128: the lists of 64 RG rows fill the LDS).
-// Quad lists with two row groups (RG = 2): 4 wavefronts of 32 query rows each, one
-// wavefront per SIMD (the lists of 32 rows take 100 VGPRs at top 100): every V tile
-// read from LDS feeds two MFMAs per k-step (as the top <= 16 kernel's two groups),
-// half the B-operand reads per score of RG = 1.
-__host__ __device__ constexpr int tk_nw(int topr, int rg = 1) {
-  return topr > 16 && rg == 2 ? 4 : (topr > 0 ? 8 : 4);
-}
+// (Quad lists with two row groups, one wavefront per SIMD, measured round 4 at
+// configs[4]'s 262,144-user sample: top-100 390 ms vs 233 ms with one group.)
+__host__ __device__ constexpr int tk_nw(int topr) { return topr > 0 ? 8 : 4; }
 template <int NK, int RG, int TOPR, int MODE = 0>
-__global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
+__global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
                                                          const uint4* __restrict__ Vlo,
                                                          const int32_t* __restrict__ perm,
@@ -509,7 +502,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const 
                                                          const float* __restrict__ scal,
                                                          int32_t* __restrict__ idx_out,
                                                          float* __restrict__ score_out) {
-  constexpr int NW = tk_nw(TOPR, RG);  // wavefronts
+  constexpr int NW = tk_nw(TOPR);  // wavefronts
   constexpr int NT = 64 * NW;          // threads
   constexpr int GR = 16 * NW;          // query rows of a row group
   constexpr int KQ = 32 * NK;
@@ -593,7 +586,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const 
   // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
   // sub-list of row m (every lane: sub-list q)
   constexpr bool QUAD = TOPR > 16;
-  static_assert(!QUAD || ((RG == 1 || RG == 2) && TOPR % 4 == 0), "quad lists: 1 or 2 row groups");
+  static_assert(!QUAD || (RG == 1 && TOPR % 4 == 0), "quad lists: one row group");
   // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
   constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
   constexpr int KG = QUAD ? RG : 1;  // quad: one sub-list per row group in every lane
@@ -653,23 +646,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const 
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
     }
   };
-  // One wavefront per SIMD (quad lists, two row groups): no partner wave hides the LDS
-  // latency of the B operands, so they are read one block ahead into registers
-  // (ALS_TK_BPREF, A/B under test).
-  constexpr bool BPREF = QUAD && RG == 2 && ALS_TK_BPREF;
-  auto load_b = [&](const uint4* tb, tk_half8 (&bh)[NK]) {
-#pragma unroll
-    for (int s = 0; s < NK; ++s) bh[s] = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
-  };
-  auto score_b = [&](const tk_half8 (&bh)[NK], floatx4 (&acc)[RG]) {
-#pragma unroll
-    for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < NK; ++s)
-#pragma unroll
-      for (int g = 0; g < RG; ++g)
-        acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh[s], acc[g], 0, 0, 0);
-  };
+
   // + hi.lo + lo.hi.  The lo halves of the block's V rows come from the lo plane in
   // global memory (only blocks past the coarse filter need them), by LDS-DMA into the
   // wave's scratch: each lane reads back the 16 B it loaded, and no VGPR holds them.
@@ -890,39 +867,17 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR, RG)) void topk_split_kernel(const 
       if (!wdone) {
         if constexpr (MODE == 3) ++n_tiles;
         floatx4 acc0[RG], acc1[RG];
-        if constexpr (BPREF) {
-          // B operands of block c+2 in flight while blocks c, c+1 are scored / filtered
-          static_assert(NC % 2 == 0, "block pairs");
-          tk_half8 bA[NK], bB[NK];
-          load_b(tb + m * RS, bA);
-          load_b(tb + (16 + m) * RS, bB);
-          score_b(bA, acc0);
+        score(tb + m * RS, acc0);
+        // block pairs: issue block c+1's MFMAs, then filter block c
 #pragma unroll 1
-          for (int c = 0; c < NC; c += 2) {
-            const uint4* tbr = tb + (16 * c + m) * RS;
-            const int* bp = tperm + buf * VT + 16 * c;
-            score_b(bB, acc1);
-            if (c + 2 < NC) load_b(tbr + 32 * RS, bA);
-            filter(acc0, vb + 16 * c, bp, tbr);
-            if (c + 2 < NC) {
-              score_b(bA, acc0);
-              load_b(tbr + 48 * RS, bB);
-            }
+        for (int c = 0; c < NC; c += 2) {
+          const uint4* tbr = tb + (16 * c + m) * RS;
+          const int* bp = tperm + buf * VT + 16 * c;
+          if (NC > 1) score(tbr + 16 * RS, acc1);
+          filter(acc0, vb + 16 * c, bp, tbr);
+          if (NC > 1) {
+            if (c + 2 < NC) score(tbr + 32 * RS, acc0);
             filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
-          }
-        } else {
-          score(tb + m * RS, acc0);
-          // block pairs: issue block c+1's MFMAs, then filter block c
-#pragma unroll 1
-          for (int c = 0; c < NC; c += 2) {
-            const uint4* tbr = tb + (16 * c + m) * RS;
-            const int* bp = tperm + buf * VT + 16 * c;
-            if (NC > 1) score(tbr + 16 * RS, acc1);
-            filter(acc0, vb + 16 * c, bp, tbr);
-            if (NC > 1) {
-              if (c + 2 < NC) score(tbr + 32 * RS, acc0);
-              filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
-            }
           }
         }
       }
@@ -1057,14 +1012,8 @@ static bool topk_quad(int top, int64_t n_v) {
   return top > kTopR && top <= kTopQ;
 }
 
-// Quad lists with two row groups per wavefront (tk_nw): A/B under test.
-#ifndef ALS_TK_QUAD_RG
-#define ALS_TK_QUAD_RG 1
-#endif
-constexpr int kTkQuadRg = ALS_TK_QUAD_RG;
-
 static int topk_nw(int top, bool quad, int rg) {
-  return quad ? tk_nw(kTopQ, rg) : (top <= kTopR ? tk_nw(1) : tk_nw(0));
+  return quad ? tk_nw(kTopQ) : (top <= kTopR ? tk_nw(1) : tk_nw(0));
 }
 
 static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
@@ -1093,7 +1042,7 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 constexpr int64_t kTkRg2MinRows = 4 * 256 * 256;
 static int topk_split_rg(int k, int top, bool quad, int64_t n_q) {
   const int kq = topk_kq(k);
-  if (quad) return kTkQuadRg;  // quad lists: one row group, or two (4 wavefronts)
+  if (quad) return 1;  // quad lists: one row group
   if (top <= kTopR && n_q < kTkRg2MinRows) return 1;
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
@@ -1200,16 +1149,16 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
     else if (!quad)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
-    else if (rg != kTkQuadRg)                         \
+    else if (rg != 1)                                 \
       return ALS_EUNSUPPORTED;                        \
     else if (top <= 32)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, 32);      \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 32);              \
     else if (top <= 64)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, 64);      \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 64);              \
     else if (top <= 100)                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, 100);     \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 100);             \
     else                                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, kTkQuadRg, kTopQ);   \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, kTopQ);           \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);

@@ -117,7 +117,8 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * LAUNCH2 = heavy-row reduce + solve, RESCUE = re-solve of the rows that missed
  * the split window (below).  They run in the order PREP, RSCALE, LAUNCH1, DUAL,
  * LAUNCH2, RESCUE; split across calls, issue them in that order on one stream
- * with the same workspace (PREP starts an empty rescue list; RESCUE empties it).  Blocks that share Y_src (row chunks of one half-sweep) may share
+ * with the same workspace (PREP starts an empty rescue list; RESCUE empties it
+ * again, so every LAUNCH1 ... RESCUE sequence needs its RESCUE).  Blocks that share Y_src (row chunks of one half-sweep) may share
  * one PREP: it sits at a fixed workspace offset (size the workspace for the
  * largest n_chunks and n_rows).
  * Split window (explicit): the Gram/rhs split uses one power-of-two scale per

@@ -1897,8 +1897,12 @@ __global__ __launch_bounds__(256) void absmax_csr_kernel(const int64_t* __restri
 }
 
 // max |x| over n floats -> *out (as ordered uint bits; *out zeroed beforehand).
+// (zero_word[0..1], when given, are cleared by block 0: the rescue count and its
+// finished-block counter for the half-sweep this prep starts, without a memset)
 __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x, int64_t n,
-                                                     unsigned* __restrict__ out) {
+                                                     unsigned* __restrict__ out,
+                                                     unsigned* __restrict__ zero_word) {
+  if (zero_word != nullptr && blockIdx.x == 0 && threadIdx.x < 2) zero_word[threadIdx.x] = 0u;
   float m = 0.f;
   const int64_t n4 = n >> 2;
   const float4* x4 = reinterpret_cast<const float4*>(x);
@@ -2480,7 +2484,7 @@ __global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const float* __restrict__ Y, int ld, int k, float reg,
     float alpha, const double* __restrict__ yty, float* __restrict__ X,
-    int32_t* __restrict__ status, const unsigned* __restrict__ rescue_cnt,
+    int32_t* __restrict__ status, unsigned* __restrict__ rescue_cnt,
     const int32_t* __restrict__ rescue_list) {
   constexpr int NPMAX = kMaxRank * (kMaxRank + 1) / 2;
   __shared__ double Ap[NPMAX];  // lower-packed A
@@ -2589,6 +2593,17 @@ __global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
       for (int d = tid; d < ld; d += kRescueThreads) xrow[d] = d < k ? (float)bs[d] : 0.f;
     }
     __syncthreads();  // LDS reused by the next listed row
+  }
+  // the list is consumed: the last block to finish (every block read the count before
+  // its increment) empties it for the next LAUNCH1 of this workspace.  rescue_cnt[1] is
+  // the finished-block counter (zeroed with the count by the prep, reset here).
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    if (atomicAdd(rescue_cnt + 1, 1u) == gridDim.x - 1) {
+      rescue_cnt[0] = 0u;
+      rescue_cnt[1] = 0u;
+    }
   }
 }
 
@@ -2808,9 +2823,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
                                                     slot_bytes(k, n_chunks));
   unsigned* rescue_cnt = scal_u + 2;
-  // the rescue list starts empty at each Y prep (a fresh workspace holds garbage) and is
-  // emptied again after each RESCUE launch (row chunks of one half-sweep share one prep)
-  if (phases & ALS_PHASE_PREP) ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));
+  // the rescue list (count at scale word 2, the rescue launch's finished-block counter
+  // at word 3) starts empty at each Y prep (cleared by the prep's absmax launch: a fresh
+  // workspace holds garbage) and is emptied by the RESCUE launch that consumes it, so the
+  // next row chunk of a half-sweep that shares one prep starts empty too
+  if ((phases & ALS_PHASE_PREP) && n_src * (int64_t)ld == 0)
+    ALS_HIP(hipMemsetAsync(rescue_cnt, 0, 2 * sizeof(unsigned), st));
   const int cn = cn_for_k(k);
   const int kp = als_k_pad(k);
   const int zero_row = (int)n_src;
@@ -2823,7 +2841,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     const int64_t ny = n_src * (int64_t)ld;
     if (ny > 0) {
       const int gy = (int)std::min<int64_t>(1024, (ny / 4 + 255) / 256 + 1);
-      absmax_kernel<<<gy, 256, 0, st>>>(Y_src, ny, scal_u);
+      absmax_kernel<<<gy, 256, 0, st>>>(Y_src, ny, scal_u, rescue_cnt);
       ALS_LAUNCH_CHECK();
     }
     if (!implicit) {
@@ -2878,7 +2896,6 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
           row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rescue_cnt, \
           rescue_list);                                                                           \
       ALS_LAUNCH_CHECK();                                                                         \
-      ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));                               \
     }                                                                                             \
   } while (0)
 #define ALS_SOLVE_W1_LAUNCH(IMP)                                                                  \
@@ -2912,7 +2929,6 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
           row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rescue_cnt, \
           rescue_list);                                                                           \
       ALS_LAUNCH_CHECK();                                                                         \
-      ALS_HIP(hipMemsetAsync(rescue_cnt, 0, sizeof(unsigned), st));                               \
     }                                                                                             \
   } while (0)
   if (implicit) {

@@ -1788,6 +1788,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
 
 // (k <= 64 keeps one gather step in flight: two steps need 187 registers, i.e. two
 // waves per SIMD instead of three, measured slower on configs[1]: 2.07 -> 2.24 ms/iter.)
+// (Four waves per SIMD for explicit k <= 64 spill 49 registers: 2.76 vs 2.25 ms/iter.)
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,

@@ -29,8 +29,9 @@ Every workload carries a roofline of its dominant kernel — ONE kernel: the pri
 gram + solve launch of each half-sweep (ALS_PHASE_LAUNCH1), timed alone with HIP
 events on the launching stream; the dual-path launch of the short rows
 (ALS_PHASE_DUAL) is timed and reported beside it (`dual`).  `frac` = algorithmic
-bytes per launch / event time / 8 TB/s; the same over the rocprofv3 kernel-trace
-average (`frac_rocprof`); the PMC traffic / counter DRAM fraction / busy fractions
+bytes per launch / event time / 8 TB/s; the same over the kernel-trace average of
+the PMC profiling runs (`frac_pmc_profile`: tools/gpu_pmc_r04.sh, `bench.py --only W
+--steps 3`, a different and shorter run than this one); the PMC traffic / counter DRAM fraction / busy fractions
 / limiter of that workload's own profiled launches (profiles/pmc_summary.json,
 keyed by workload, kernel and grid size).  `cpu_baseline`: the C port of Spark's
 per-row dspr + dppsv arithmetic (oracle/als_oracle.c) on every host core in this
@@ -190,8 +191,8 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
     phase).  launches: {"item"|"user": {"ms": HIP-event average of the phase on the
     launching stream, "nnz": ratings, "rows": rows solved in the phase, "parts":
     [(kernel, grid threads)]}}.  achieved = algorithmic bytes (or modelled issued flops:
-    the primal k x k Gram + solve for every row) / event time; frac_rocprof uses the
-    rocprofv3 kernel-trace durations of the same kernels instead; traffic / busy
+    the primal k x k Gram + solve for every row) / event time; frac_pmc_profile uses the
+    kernel-trace durations of the same kernels in the PMC profiling runs; traffic / busy
     fractions / limiter / counted MFMA flops come from that workload's PMC passes."""
     out = {"kernel": kernel, "launches": {}}
     tb = tf = tfa = te = tr = 0.0
@@ -214,8 +215,8 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
                 ent["mfma_issued_flops_pmc"] = pv["mfma_flop_f16"]
                 ent["mfma_frac_pmc"] = pv["mfma_flop_f16"] / t / 1e12 / PEAK_F16_MFMA_TFLOPS
             if pv.get("trace_avg_ns"):
-                ent["rocprof_ms"] = pv["trace_avg_ns"] * 1e-6
-                ent["hbm_frac_rocprof"] = b / (pv["trace_avg_ns"] * 1e-9) / 1e9 / PEAK_HBM_GBS
+                ent["pmc_profile_trace_ms"] = pv["trace_avg_ns"] * 1e-6
+                ent["hbm_frac_pmc_profile"] = b / (pv["trace_avg_ns"] * 1e-9) / 1e9 / PEAK_HBM_GBS
                 tr += pv["trace_avg_ns"] * 1e-9
             else:
                 have_trace = False
@@ -271,9 +272,9 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
                 "frac": view["frac"],
                 "traffic": traffic / n if (have_traffic and traffic > 0) else None})
     if have_trace and tr > 0:
-        out["frac_rocprof"] = (tb / tr / 1e9 / PEAK_HBM_GBS) if bound == "hbm" else \
+        out["frac_pmc_profile"] = (tb / tr / 1e9 / PEAK_HBM_GBS) if bound == "hbm" else \
             (tf / tr / 1e12 / PEAK_F16_MFMA_TFLOPS)
-        out["rocprof_avg_launch_us"] = 1e6 * tr / n
+        out["pmc_profile_avg_launch_us"] = 1e6 * tr / n
     return out
 
 
@@ -322,7 +323,7 @@ def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int
             out["achieved"] = out["issued_f16_mfma_tflops_pmc"]
             out["frac"] = out["achieved"] / PEAK_F16_MFMA_TFLOPS
         if pv.get("trace_avg_ns"):
-            out["rocprof_ms"] = pv["trace_avg_ns"] * 1e-6
+            out["pmc_profile_trace_ms"] = pv["trace_avg_ns"] * 1e-6
         if "limiter" in pv:
             out["limiter"] = pv["limiter"]
     return out

@@ -69,10 +69,10 @@ def test_phase_counters_combine_by_grid(bench, monkeypatch):
     r = bench.roofline("w", "k", {"user": {"ms": 4.0, "nnz": 10 ** 6, "rows": 1000, "parts": parts}},
                        128, False)
     u = r["launches"]["user"]
-    assert u["rocprof_ms"] == pytest.approx(4.0)
+    assert u["pmc_profile_trace_ms"] == pytest.approx(4.0)
     assert u["mfma_issued_flops_pmc"] == pytest.approx(1.2e12)
     assert r["traffic"] == pytest.approx(6.2e9)
-    assert r["frac_rocprof"] == pytest.approx(r["frac"])  # same duration here
+    assert r["frac_pmc_profile"] == pytest.approx(r["frac"])  # same duration here
 
 
 @pytest.mark.parametrize("k,top,n_q,kern,grid", [

@@ -1277,6 +1277,82 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& dse
   return dmin;
 }
 
+// x of row group G broadcast to all four row groups (two VALU lane swaps:
+// v_permlane32_swap gives rows {0,1} (or {2,3}) in both halves, v_permlane16_swap then
+// row 2h (or 2h+1) in all four).
+template <int G>
+__device__ __forceinline__ float rowgroup_bcast(float x) {
+  uint32_t a = __builtin_bit_cast(uint32_t, x), b = a;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  uint32_t c = G < 2 ? a : b, d = c;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
+  return __builtin_bit_cast(float, (G & 1) ? d : c);
+}
+
+// v on the lanes of 64-bit mask M (a constant), else w.
+template <uint64_t M>
+__device__ __forceinline__ float sel_mask(float v, float w) {
+  float r;
+  asm volatile("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(v), "v"(w), "s"(M));
+  return r;
+}
+
+// The sweep of sweep16 on a symmetric 16 x 16 block held in the MFMA C layout (lane
+// (q, m): B[4q + r][m], r = 0..3) instead of column per lane: per pivot p, row p is
+// broadcast from row group p/4 to all four (rowgroup_bcast), and a lane's four column-p
+// entries come from lane p of its own row group (v_fmac_f32_dpp row_newbcast:p), so a
+// lane updates its four entries, not sixteen replicated ones, and the block never goes
+// through LDS (the result is already in the C layout the Pm / Schur MFMAs read).  Every
+// entry sees the same fp32 operations, in the same order, as in sweep16 (deferred
+// pivot-column scaling, look-ahead of the next pivot).
+template <class Hook>
+__device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
+  // Bv was just written by the matrix cores (the pivot block's Schur update) and is
+  // read below by inline DPP asm, which the hazard recognizer does not see: the XDL
+  // write -> VALU read wait states by hand (tests/test_isa_hazards.py checks the rest)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  float B[4] = {Bv[0], Bv[1], Bv[2], Bv[3]};
+  float dmin = 3.0e38f;
+  float dself = 1.f;
+  float rowp = rowgroup_bcast<0>(B[0]);
+  float d = bcast16<0>(rowp);
+  float rd = rcp_t(d);
+  float f = rowp * rd;
+  float nf = sel_lane16<0>(0.f, -f);
+  static_for<16>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
+    dmin = fminf(dmin, d);
+    asm volatile("s_nop 1" ::: "memory");
+    // the register holding row p+1 first: then pivot p+1's row is final
+    fmac_bcast16<p>(B[rn], nf);
+    float dn = 0.f, rdn = 0.f, fn = 0.f, nfn = 0.f;
+    if constexpr (p + 1 < 16) {
+      constexpr int qn = (p + 1) >> 2;
+      const float rown = rowgroup_bcast<qn>(B[rn]);
+      dn = bcast16<p + 1>(rown);
+      rdn = rcp_t(dn);
+      fn = rown * rdn;
+      nfn = sel_lane16<p + 1>(0.f, -fn);
+    }
+    static_for<4>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if constexpr (r != rn) fmac_bcast16<p>(B[r], nf);
+    });
+    // row p (row group qp): f off the pivot, -1 on it (scaled by 1/d at the end)
+    B[rp] = sel_mask<0xFFFFull << (16 * qp)>(sel_lane16<p>(-1.f, f), B[rp]);
+    dself = sel_lane16<p>(d, dself);
+    hook(pc);
+    d = dn; rd = rdn; f = fn; nf = nfn;
+  });
+  const float s = rcp_t(dself);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Bv[r] = B[r] * s;
+  dself_out = dself;
+  return dmin;
+}
+
+
 // Schur tiles of step K, I-major: u = 0 is (K+1, K+1), the next pivot block.
 template <int NB>
 __host__ __device__ constexpr int schur_n(int K) { return (NB - 1 - K) * (NB - K) / 2; }
@@ -1315,6 +1391,14 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 // 8.1 ms/iter measured).
 template <int NB>
 constexpr bool kW1SplitSchur = NB == 8;
+// Diagonal blocks swept in the MFMA C layout (sweep16c: 4 entries per lane instead of
+// 16 replicated) where the register file has room: the k <= 64 solves and the n x n
+// dual systems (A/B round 4: configs[1] 2.26 -> 2.21 ms/iter, configs[3] dual 70.4 ->
+// 68.0 ms).  Not in the NB = 8 (W1) kernels: there the compiler keeps tiles in AGPRs and
+// copies them out right before the inline DPP asm, a hazard it does not see (2.2e-2
+// row errors measured).
+template <int NB>
+constexpr bool kSweepC = NB <= 6;
 // Measured round 4 (A/B at configs[1] / configs[3]): the split form in the explicit
 // k <= 64 solve (2.33 vs 2.26 ms/iter), the explicit rank-128 light rows (user launch
 // 112 vs 102 ms) and the n x n dual systems (76 vs 70 ms) is slower: fp32 stays there.
@@ -1498,6 +1582,19 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   floatx4 Gm, bk;
   auto pivot_block = [&](auto Kc, auto&& hook) {
     constexpr int K = decltype(Kc)::value;
+    if constexpr (kSweepC<NB>) {
+      // swept in the C layout: Gm comes out where the MFMAs read it
+      Gm = A[w1_tile<NB>(K, K)];
+      float ds;
+      dmin = fminf(dmin, sweep16c(Gm, hook, ds));
+      track_pivot(ds, m * NB + K < k);
+      const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
+      if (q == 0) vec[m] = bK;
+      wave_lds_order();
+      bk = *reinterpret_cast<const floatx4*>(vec + 4 * q);  // row layout
+      wave_lds_order();
+      return;
+    }
     *reinterpret_cast<floatx4*>(col + m * CS + 4 * q) = A[w1_tile<NB>(K, K)];
     wave_lds_order();
     float R[16];

@@ -1392,13 +1392,14 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 template <int NB>
 constexpr bool kW1SplitSchur = NB == 8;
 // Diagonal blocks swept in the MFMA C layout (sweep16c: 4 entries per lane instead of
-// 16 replicated) where the register file has room: the k <= 64 solves and the n x n
-// dual systems (A/B round 4: configs[1] 2.26 -> 2.21 ms/iter, configs[3] dual 70.4 ->
-// 68.0 ms).  Not in the NB = 8 (W1) kernels: there the compiler keeps tiles in AGPRs and
+// 16 replicated) for NB = 4: the k <= 64 solves and the 33-64-rating dual systems
+// (A/B round 4, `profiles/r04/ab_sweepc_classes.jsonl`: configs[1] 2.246 -> 2.203
+// ms/iter, configs[3] 294.6 -> 292.8 ms; with NB = 2 and 6 as well configs[3] went to
+// 299).  Never in the NB = 8 (W1) kernels: there the compiler keeps tiles in AGPRs and
 // copies them out right before the inline DPP asm, a hazard it does not see (2.2e-2
-// row errors measured).
+// row errors measured; tests/test_isa_hazards.py scans for it).
 template <int NB>
-constexpr bool kSweepC = NB <= 6;
+constexpr bool kSweepC = NB == 4;
 // Measured round 4 (A/B at configs[1] / configs[3]): the split form in the explicit
 // k <= 64 solve (2.33 vs 2.26 ms/iter), the explicit rank-128 light rows (user launch
 // 112 vs 102 ms) and the n x n dual systems (76 vs 70 ms) is slower: fp32 stays there.

@@ -274,7 +274,11 @@ class ShardedALS:
     # ---- setup helpers ----
     def _auto_chunks(self, u_space: int, i_space: int) -> int:
         """4 row chunks when a rank's share of the larger id space reaches 1M rows
-        (the all-gather then moves >= 256 MB per rank at rank 64), else 1; and at
+        (the all-gather then moves >= 256 MB per rank at rank 64); 2 from 4 ranks on
+        when the share reaches 64k rows (the weak-scaled configs[1] shape: at 8 ranks
+        each receives ~290 MB of U per iteration, about the half-sweep's own time on a
+        ring over xGMI, so chunk 0's gather hides behind chunk 1's solve — a model
+        choice, the 1-rank cost of the second chunk is +0.15 ms); else 1; and at
         least enough chunks that one chunk's all-gather stays within
         MAX_COLLECTIVE_BYTES: a chunk holds at most ceil(PAD_CAP n / (W C)) rows of each
         rank (the cap _layout applies), so the all-gather of one chunk moves at most
@@ -282,7 +286,7 @@ class ShardedALS:
         _solve_and_gather never stops a configuration more chunks would handle."""
         big = max(u_space, i_space)
         W = self.world
-        c = max(1, 4 if (W > 1 and big // W >= (1 << 20)) else 1)
+        c = 4 if (W > 1 and big // W >= (1 << 20)) else (2 if (W >= 4 and big // W >= (1 << 16)) else 1)
         # (a chunk of one row per rank is the floor: below it the guard decides, with
         # the real row size)
         while (math.ceil(PAD_CAP * big / (W * c)) > 1 and

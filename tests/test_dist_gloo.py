@@ -480,7 +480,9 @@ def test_padding_bounded_with_popularity_ordered_ids(tmp_path, world):
 def test_auto_chunks_keep_every_chunk_gather_within_the_cap():
     """_auto_chunks counts a chunk's all-gather exactly (W x the per-chunk row cap x
     512 B), for world sizes that are not powers of two too, and adds no chunk beyond
-    what the cap needs."""
+    what the cap needs.  Floors: 4 chunks from 1M rows per rank, 2 from 64k rows per
+    rank at 4+ ranks (the weak-scaled configs[1] shape: chunk 0's all-gather hides
+    behind chunk 1's solve), else 1."""
     import math
     from types import SimpleNamespace
     import _pkgload
@@ -491,7 +493,9 @@ def test_auto_chunks_keep_every_chunk_gather_within_the_cap():
             c = Dm.ShardedALS._auto_chunks(SimpleNamespace(world=W), big, 7)
             rows = math.ceil(Dm.PAD_CAP * big / (W * c))
             assert W * rows * 512 <= Dm.MAX_COLLECTIVE_BYTES, (W, big, c)
-            floor = 4 if (W > 1 and big // W >= (1 << 20)) else 1
+            floor = 4 if (W > 1 and big // W >= (1 << 20)) else \
+                (2 if (W >= 4 and big // W >= (1 << 16)) else 1)
+            assert c >= floor
             if c > floor:  # one chunk fewer would break the cap
                 assert W * math.ceil(Dm.PAD_CAP * big / (W * (c - 1))) * 512 > \
                     Dm.MAX_COLLECTIVE_BYTES

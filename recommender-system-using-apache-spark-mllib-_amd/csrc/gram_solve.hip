@@ -1395,9 +1395,11 @@ constexpr bool kW1SplitSchur = NB == 8;
 // 16 replicated) for NB = 4: the k <= 64 solves and the 33-64-rating dual systems
 // (A/B round 4, `profiles/r04/ab_sweepc_classes.jsonl`: configs[1] 2.246 -> 2.203
 // ms/iter, configs[3] 294.6 -> 292.8 ms; with NB = 2 and 6 as well configs[3] went to
-// 299).  Never in the NB = 8 (W1) kernels: there the compiler keeps tiles in AGPRs and
+// 299).  Not in the NB = 8 (W1) kernels: there the compiler keeps tiles in AGPRs and
 // copies them out right before the inline DPP asm, a hazard it does not see (2.2e-2
-// row errors measured; tests/test_isa_hazards.py scans for it).
+// row errors measured; tests/test_isa_hazards.py scans for it), and with a nop in
+// front of every DPP statement they measured slower (configs[2] 9.03 -> 11.56 ms,
+// configs[3] 293 -> 300 ms, `profiles/r04/ab_sweepc_w1.jsonl`).
 template <int NB>
 constexpr bool kSweepC = NB == 4;
 // Measured round 4 (A/B at configs[1] / configs[3]): the split form in the explicit

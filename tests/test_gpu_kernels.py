@@ -387,6 +387,47 @@ def test_split_window_row_norm_spread(spread, rank):
     assert eu.max() <= 1e-4
 
 
+def test_rescue_list_emptied_between_row_chunks():
+    """Row chunks of one half-sweep share one Y prep (the sharded engine's chunk calls run
+    every phase but PREP): the rescue list a call fills must be empty again when the next
+    call's LAUNCH1 starts (the rescue launch's last block clears it), or rows of one
+    chunk would be re-solved with the next chunk's CSR.  Counted directly: the list
+    length (scale word 2) after LAUNCH1..LAUNCH2 is the same in both calls, and 0 after
+    RESCUE."""
+    rank, spread = 64, 1e9
+    u1, i1, r1 = planted(500, 300, density=0.05, heavy_items=(3,), seed=31)
+    u2, i2, r2 = planted(400, 120, density=0.08, heavy_items=(5,), seed=32)
+    u = np.concatenate([u1, u2 + 500]).astype(np.int32)
+    i = np.concatenate([i1, i2 + 300]).astype(np.int32)
+    r = np.concatenate([r1, r2]).astype(np.float32)
+    core = _core(u, i, r, chunk=128)
+    core.init_factors(rank, seed=3)
+    core.U[500:] /= spread
+    U0 = core.U[:, :rank].cpu().numpy()
+    ib = core.item_block
+    V_ref = O.half_sweep(ib.row_ptr.cpu().numpy(), ib.col.cpu().numpy(), ib.val.cpu().numpy(),
+                         U0, 0.1)
+
+    def count():
+        torch.cuda.synchronize()
+        return int(core.ws.buf[8:12].view(torch.int32).item())
+    counts = []
+    for phases in (E.PHASE_ALL, E.PHASE_ALL & ~E.PHASE_PREP):
+        core.V.fill_(7.0)
+        core.status.zero_()
+        E.solve_half(ib, core.U, core.V, rank, 0.1, False, 1.0, None, core.status, core.ws,
+                     phases & ~E.PHASE_RESCUE)
+        counts.append(count())
+        E.solve_half(ib, core.U, core.V, rank, 0.1, False, 1.0, None, core.status, core.ws,
+                     E.PHASE_RESCUE)
+        assert count() == 0
+        core.check_status()
+        e = _exact_rel_errs(core.V[:, :rank].cpu().numpy(), V_ref)
+        assert e.max() <= 1e-4, (phases, float(e.max()))
+    report("rescue_list_between_chunks", {"rescued_per_call": counts})
+    assert counts[0] > 0 and counts[0] == counts[1], counts
+
+
 @pytest.mark.parametrize("rank", [8, 64, 128])
 def test_split_window_rating_spread(rank):
     """Ratings spanning nine decades: users whose ratings are all ~1e-9 of the block's

@@ -1860,6 +1860,34 @@ __device__ __forceinline__ void add_slot(const double* __restrict__ slot, double
   npos += (int)slot[(N * 4 + NRA) * 64 + lane];
 }
 
+// The same slot as fp32 (a chunk task's sums are fp32 anyway: storing them as fp64
+// only doubled the launch-1 write and launch-2a read bytes of the k <= 64 heavy rows).
+template <int N, int NRA>
+__device__ __forceinline__ void store_slot_f32(float* __restrict__ slot, const float (&tot)[N][4],
+                                               const float (&bt)[NRA], float npos) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slot[(t * 4 + r) * 64 + lane] = tot[t][r];
+#pragma unroll
+  for (int c = 0; c < NRA; ++c) slot[(N * 4 + c) * 64 + lane] = bt[c];
+  slot[(N * 4 + NRA) * 64 + lane] = npos;
+}
+
+template <int N, int NRA>
+__device__ __forceinline__ void add_slot_f32(const float* __restrict__ slot, double (&a64)[N][4],
+                                             double (&b64)[NRA], int& npos) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a64[t][r] += (double)slot[(t * 4 + r) * 64 + lane];
+#pragma unroll
+  for (int c = 0; c < NRA; ++c) b64[c] += (double)slot[(N * 4 + c) * 64 + lane];
+  npos += (int)slot[(N * 4 + NRA) * 64 + lane];
+}
+
 template <int N, int NRA, class AccT>
 __device__ __forceinline__ void zero_acc(AccT (&tot)[N][4], AccT (&bt)[NRA]) {
 #pragma unroll
@@ -1896,7 +1924,7 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const int32_t* __restrict__ chunk_row, const int64_t* __restrict__ chunk_begin,
     const int64_t* __restrict__ chunk_end, int32_t n_chunks, int32_t n_light,
     const float* __restrict__ Y, float* __restrict__ X, int ld, int k, float reg, float alpha,
-    const double* __restrict__ yty, double* __restrict__ slots, int32_t* __restrict__ status,
+    const double* __restrict__ yty, float* __restrict__ slots, int32_t* __restrict__ status,
     const float* __restrict__ scal, const uint32_t* __restrict__ Ysp, int32_t kp,
     int32_t zero_row, unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
   constexpr int NT = Cfg<CN>::NT;
@@ -1951,8 +1979,8 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
   if (chunk >= 0) {
     // explicit: the npos entry carries the chunk's scaled max |rating| (launch 2 takes
     // the max over the chunks for the window guard)
-    store_slot<NT, CN, float>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt,
-                              IMPLICIT ? (float)npos : rmax);
+    store_slot_f32<NT, CN>(slots + (int64_t)chunk * Cfg<CN>::SLOT, tot, bt,
+                           IMPLICIT ? (float)npos : rmax);
     return;
   }
   __syncthreads();  // staging area is reused by the solve
@@ -2016,40 +2044,40 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
 }
 
 // Launch 2: heavy rows — sum their chunk slots in a fixed order (fp64), then solve.
-// Launch 2a (k <= 64): a heavy row's fp64 chunk slots summed element-wise (one
-// thread per slot element, four interleaved partial sums in a fixed order) into its
-// first slot; each thread reads and writes only its own element.
+// Launch 2a (k <= 64): a heavy row's fp32 chunk slots summed element-wise in fp64 (one
+// thread per slot element, four interleaved partial sums in a fixed order), rounded
+// once to fp32 into its first slot; each thread reads and writes only its own element.
 // Explicit: the last 64 entries (each chunk's scaled max |rating|) take the max.
 template <int SLOT, bool IMPLICIT>
 __global__ __launch_bounds__(256) void heavy_sum_f64_kernel(const int32_t* __restrict__ slot_begin,
-                                                            double* __restrict__ slots) {
+                                                            float* __restrict__ slots) {
   const int h = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= SLOT) return;
   const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
   if (s1 - s0 <= 1) return;
   if (!IMPLICIT && e >= SLOT - 64) {
-    double mx = 0.0;
-    for (int s = s0; s < s1; ++s) mx = fmax(mx, slots[(int64_t)s * SLOT + e]);
+    float mx = 0.f;
+    for (int s = s0; s < s1; ++s) mx = fmaxf(mx, slots[(int64_t)s * SLOT + e]);
     slots[(int64_t)s0 * SLOT + e] = mx;
     return;
   }
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   int s = s0;
   for (; s + 4 <= s1; s += 4) {
-    a0 += slots[(int64_t)s * SLOT + e];
-    a1 += slots[(int64_t)(s + 1) * SLOT + e];
-    a2 += slots[(int64_t)(s + 2) * SLOT + e];
-    a3 += slots[(int64_t)(s + 3) * SLOT + e];
+    a0 += (double)slots[(int64_t)s * SLOT + e];
+    a1 += (double)slots[(int64_t)(s + 1) * SLOT + e];
+    a2 += (double)slots[(int64_t)(s + 2) * SLOT + e];
+    a3 += (double)slots[(int64_t)(s + 3) * SLOT + e];
   }
-  for (; s < s1; ++s) a0 += slots[(int64_t)s * SLOT + e];
-  slots[(int64_t)s0 * SLOT + e] = (a0 + a1) + (a2 + a3);
+  for (; s < s1; ++s) a0 += (double)slots[(int64_t)s * SLOT + e];
+  slots[(int64_t)s0 * SLOT + e] = (float)((a0 + a1) + (a2 + a3));
 }
 
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
-    const int32_t* __restrict__ slot_begin, const double* __restrict__ slots,
+    const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status, const float* __restrict__ scal,
     unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
@@ -2061,8 +2089,8 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
   // the row's chunk slots were summed into its first slot (heavy_sum_f64_kernel)
-  const double* sl = slots + (int64_t)slot_begin[h] * Cfg<CN>::SLOT;
-  add_slot<NT, CN>(sl, a64, b64, npos);
+  const float* sl = slots + (int64_t)slot_begin[h] * Cfg<CN>::SLOT;
+  add_slot_f32<NT, CN>(sl, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
   if constexpr (!IMPLICIT) {  // split window guard over the whole row
     const float s2 = ldexpf(1.f, 2 * split_exponent(scal[0]));
@@ -2843,15 +2871,20 @@ int32_t als_k_pad(int32_t k) { return 16 * cn_for_k(k); }
 
 static size_t slot_doubles(int k) {  // partial slot of one heavy-row chunk (solve)
   switch (cn_for_k(k)) {
-    case 1: return Cfg<1>::SLOT;
-    case 2: return Cfg<2>::SLOT;
-    case 4: return Cfg<4>::SLOT;
+    case 1: return (Cfg<1>::SLOT + 1) / 2;  // fp32 chunk partials
+    case 2: return (Cfg<2>::SLOT + 1) / 2;
+    case 4: return (Cfg<4>::SLOT + 1) / 2;
     default: return (size_t)(kW1Slot + 1) / 2;  // W1 stores fp32 partials
   }
 }
 
-static size_t yty_slot_doubles(int k) {  // partial slot of one YtY task
-  return cn_for_k(k) == 8 ? (size_t)kWgSlot : slot_doubles(k);
+static size_t yty_slot_doubles(int k) {  // partial slot of one YtY task (fp64 slots)
+  switch (cn_for_k(k)) {
+    case 1: return Cfg<1>::SLOT;
+    case 2: return Cfg<2>::SLOT;
+    case 4: return Cfg<4>::SLOT;
+    default: return (size_t)kWgSlot;
+  }
 }
 
 extern "C" {
@@ -2969,11 +3002,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const bool rescue = (phases & ALS_PHASE_RESCUE) && n_rows > 0;
 #define ALS_SOLVE_LAUNCH(CN, IMP)                                                                 \
   do {                                                                                            \
+    float* slots_f = reinterpret_cast<float*>(slots);                                             \
     if (g1)                                                                                       \
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
                                                     chunk_begin, chunk_end, n_chunks,             \
                                                     n_light_primal, Y_src, X_dst, ld, k, reg,     \
-                                                    alpha, yty_packed, slots, status_dev, scal,   \
+                                                    alpha, yty_packed, slots_f, status_dev, scal,   \
                                                     Ysp, kp, zero_row, rescue_cnt, rescue_list);  \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd && CN == 4 && !IMP) {                                                                  \
@@ -2985,10 +3019,10 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_f64_kernel<Cfg<CN>::SLOT, IMP>                                                    \
-          <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots);       \
+          <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots_f);     \
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
-                                                      slots, X_dst, ld, k, reg, yty_packed,       \
+                                                      slots_f, X_dst, ld, k, reg, yty_packed,     \
                                                       status_dev, scal, rescue_cnt, rescue_list); \
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \

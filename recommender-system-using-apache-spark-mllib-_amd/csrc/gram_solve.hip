@@ -2017,10 +2017,19 @@ __global__ __launch_bounds__(256) void absmax_csr_kernel(const int64_t* __restri
   float m = 0.f;
   const int64_t n4 = n >> 2;  // val is 16-byte aligned (a CSR value array)
   const float4* v4 = reinterpret_cast<const float4*>(val);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const float4 v = v4[i];
+  auto fold = [&](const float4& v) {
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  };
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {  // four independent loads in flight
+    const float4 a = v4[i], b = v4[i + stride], c = v4[i + 2 * stride], d = v4[i + 3 * stride];
+    fold(a);
+    fold(b);
+    fold(c);
+    fold(d);
   }
+  for (; i < n4; i += stride) fold(v4[i]);
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = fmaxf(m, fabsf(val[4 * n4 + threadIdx.x]));
   block_absmax_publish(m, out);
 }
@@ -2035,10 +2044,19 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
   float m = 0.f;
   const int64_t n4 = n >> 2;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const float4 v = x4[i];
+  auto fold = [&](const float4& v) {
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  };
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {  // four independent loads in flight
+    const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+    fold(a);
+    fold(b);
+    fold(c);
+    fold(d);
   }
+  for (; i < n4; i += stride) fold(x4[i]);
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = fmaxf(m, fabsf(x[4 * n4 + threadIdx.x]));
   block_absmax_publish(m, out);
 }
@@ -2974,7 +2992,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }
     const int64_t ny = n_src * (int64_t)ld;
     if (ny > 0) {
-      const int gy = (int)std::min<int64_t>(1024, (ny / 4 + 255) / 256 + 1);
+      // 256 workgroups (one atomic each on the scale word; 1024 serialised there)
+      const int gy = (int)std::min<int64_t>(256, (ny / 4 + 255) / 256 + 1);
       absmax_kernel<<<gy, 256, 0, st>>>(Y_src, ny, scal_u, rescue_cnt);
       ALS_LAUNCH_CHECK();
     }
@@ -2992,7 +3011,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     if (n_light + n_heavy > 0) {
       ALS_REQUIRE(val != nullptr, ALS_EINVAL, "als_solve_half: null val");
       // every row is light or heavy: the block's ratings are val[0, row_ptr[n_light + n_heavy])
-      absmax_csr_kernel<<<1024, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
+      absmax_csr_kernel<<<256, 256, 0, st>>>(row_ptr, n_light + n_heavy, val, scal_u + 1);
       ALS_LAUNCH_CHECK();
     }
   }

@@ -60,10 +60,19 @@ __global__ __launch_bounds__(256) void tk_absmax_kernel(const float* __restrict_
   float m = 0.f;
   const int64_t n4 = n >> 2;
   const float4* x4 = reinterpret_cast<const float4*>(x);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const float4 v = x4[i];
+  auto fold = [&](const float4& v) {
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  };
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 3 * stride < n4; i += 4 * stride) {  // four independent loads in flight
+    const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+    fold(a);
+    fold(b);
+    fold(c);
+    fold(d);
   }
+  for (; i < n4; i += stride) fold(x4[i]);
   if (blockIdx.x == 0 && threadIdx.x < (n & 3)) m = fmaxf(m, fabsf(x[4 * n4 + threadIdx.x]));
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   __shared__ float red[4];
@@ -1131,11 +1140,11 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   const int kq_shift = __builtin_ctz(kq);
   ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
   const int64_t nq_el = n_q * (int64_t)ld, nv_el = n_v * (int64_t)ld;
-  tk_absmax_kernel<<<(int)std::min<int64_t>(1024, (nq_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
+  tk_absmax_kernel<<<(int)std::min<int64_t>(256, (nq_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
       Q, nq_el, scal_u);
   ALS_LAUNCH_CHECK();
   if (n_v > 0) {
-    tk_absmax_kernel<<<(int)std::min<int64_t>(1024, (nv_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
+    tk_absmax_kernel<<<(int)std::min<int64_t>(256, (nv_el / 4 + 255) / 256 + 1), 256, 0, st>>>(
         V, nv_el, scal_u + 1);
     ALS_LAUNCH_CHECK();
     // sweep order: V rows by decreasing norm (bucketed)

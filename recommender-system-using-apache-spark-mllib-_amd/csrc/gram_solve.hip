@@ -1016,7 +1016,20 @@ __device__ __forceinline__ void block_back_subst(int NB, const float* __restrict
   }
 }
 
+// x (permuted block layout Xv[K*16 + i] = dim i*CN + K) -> xrow (natural order, 0 past k
+// and everywhere when !ok).
 template <int CN>
+__device__ __forceinline__ void panel_store_x(const float* __restrict__ Xv, int k, bool ok,
+                                              float* __restrict__ xrow, int ld) {
+  for (int d = threadIdx.x & 63; d < ld; d += 64) {
+    const float x = d < 16 * CN ? Xv[(d % CN) * 16 + d / CN] : 0.f;
+    xrow[d] = (d < k && ok) ? x : 0.f;
+  }
+}
+
+// SPREAD: the pivot spread test (explicit rows; the implicit rows are checked a
+// posteriori by iterative refinement instead).  STORE: write x to xrow here.
+template <int CN, bool SPREAD = true, bool STORE = true>
 __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const float (&bq)[CN],
                                                 float* __restrict__ lds, int k,
                                                 float* __restrict__ xrow, int ld) {
@@ -1115,15 +1128,47 @@ __device__ __forceinline__ bool panel_ldl_solve(floatx4 (&A)[Cfg<CN>::NT], const
     pmin = fminf(pmin, __shfl_xor(pmin, o));
     pmax = fmaxf(pmax, __shfl_xor(pmax, o));
   }
-  const bool ok = __ballot(!okl) == 0 && pmax <= kCondMax * pmin;
+  const bool ok = __ballot(!okl) == 0 && (!SPREAD || pmax <= kCondMax * pmin);
   // (e) back substitution
   block_back_subst<CS>(NB, lds + Lo::T, Zv, Dv, Xv);
   // (f) un-permute: dim d = i*CN + K  <->  Xv[K*16 + i]
-  for (int d = lane; d < ld; d += 64) {
-    const float x = d < 16 * CN ? Xv[(d % CN) * 16 + d / CN] : 0.f;
-    xrow[d] = (d < k && ok) ? x : 0.f;
-  }
+  if constexpr (STORE) panel_store_x<CN>(Xv, k, ok, xrow, ld);
   return ok;
+}
+
+// Forward substitution U^T z = r for a new right-hand side (U unit upper from the
+// panel factorisation: tile slot (J, K) column i holds U_JK[p][i], p = 0..15, and the
+// diagonal tiles hold 0 on and below the diagonal), block row by block row on lanes
+// 0..15 (lanes 16.. mirror).  Rv, Zv in the permuted block layout.
+template <int CS>
+__device__ __forceinline__ void block_fwd_subst(int NB, const float* __restrict__ tiles,
+                                                const float* __restrict__ Rv,
+                                                float* __restrict__ Zv) {
+  const int lane = threadIdx.x & 63, i = lane & 15;
+  for (int K = 0; K < NB; ++K) {
+    float v = Rv[K * 16 + i];
+    for (int J = 0; J < K; ++J) {  // v -= U_JK^T z_J: column i of tile (J, K)
+      const float* U = tiles + tile_index(NB, J, K) * 16 * CS + i * CS;
+#pragma unroll
+      for (int p4 = 0; p4 < 4; ++p4) {
+        const float4 zj = *reinterpret_cast<const float4*>(Zv + J * 16 + 4 * p4);
+        v = fmaf(-U[4 * p4 + 0], zj.x, v);
+        v = fmaf(-U[4 * p4 + 1], zj.y, v);
+        v = fmaf(-U[4 * p4 + 2], zj.z, v);
+        v = fmaf(-U[4 * p4 + 3], zj.w, v);
+      }
+    }
+    const float* Ukk = tiles + tile_index(NB, K, K) * 16 * CS + i * CS;
+    float u[16];
+#pragma unroll
+    for (int p = 0; p < 16; ++p) u[p] = Ukk[p];  // U_KK[p][i]: 0 for p >= i
+    static_for<16>([&](auto pc) {  // z_i = v_i - sum_{p < i} U_KK[p][i] z_p
+      constexpr int p = decltype(pc)::value;
+      v = fmaf(-u[p], newbcast<p>(v), v);
+    });
+    if (lane < 16) Zv[K * 16 + i] = v;
+    wave_lds_sync();
+  }
 }
 
 
@@ -1503,11 +1548,23 @@ __device__ __forceinline__ bool window_miss(float diag_lane, float n_terms, floa
   return dmiss || rmiss;
 }
 
-// Append `row` to the rescue list (one lane; each row is appended at most once per
-// half-sweep, so the list never exceeds the rows of the block).
-__device__ __forceinline__ void rescue_append(unsigned* __restrict__ cnt, int32_t* __restrict__ list,
-                                              int row) {
-  if ((threadIdx.x & 63) == 0) list[atomicAdd(cnt, 1u)] = row;
+// The rescue list of one als_solve_half call: count word (scale word 2), the list
+// (cap = the call's rows) in the workspace.
+struct RescueList {
+  unsigned* cnt;
+  int32_t* list;
+  unsigned cap;
+};
+
+// Append `row` to the rescue list (one lane).  Each row is appended at most once per
+// LAUNCH1..RESCUE sequence; a caller that runs the launches twice without the RESCUE
+// phase between them overflows the count, which is never written past `cap`:
+// rescue64_kernel walks min(count, cap) entries and reports the overflow (status -1).
+__device__ __forceinline__ void rescue_append(const RescueList& rl, int row) {
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned i = atomicAdd(rl.cnt, 1u);
+    if (i < rl.cap) rl.list[i] = row;
+  }
 }
 
 // [hi | lo] f16 halves of s * x (s a power of two): hi = f16(s x) and
@@ -1764,12 +1821,146 @@ __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float 
   return ok;
 }
 
-template <int CN>
-struct SmemBytes {
-  static constexpr int value = (int)sizeof(float) * PanelLds<CN>::SIZE;
+// ---------------------------------------------------------------------------
+// Iterative refinement of the implicit rows' panel solutions (k <= 64).
+//
+// The fp32-grade Gram (split-f16 products, fp32 sums) and the fp32 LDL^T each
+// perturb A by ~2^-21..2^-24 relative, which the condition of an implicit system
+// (confidences 1 + alpha |r| spanning decades) amplifies: emulated at ranks 16-64 on
+// counts 1..1e6, 1e-4..4e-3 relative errors, half from each source.  Mixed-precision
+// refinement removes both: r = b - A x with A's own terms in Spark's fp64 arithmetic
+// (NormalEquation.add: products of fp32 values, exact in fp64; YtY; lambda n), the
+// correction A d = r solved with the kept fp32 factorisation, x += d.  Each step
+// contracts the error by ~cond(A) 2^-21, and |d| estimates the error it removed, so
+// the loop is its own a-posteriori test: done when |d| <= kIrConv |x| (the error left
+// is then ~(|d| / |x|)^2 |x| <= 1e-7 |x|), and a row that has not converged within
+// kIrSteps, or whose correction exceeds kIrDiverge |x| (contraction not reliable), is
+// re-solved in fp64 (rescue64_kernel).
+// ---------------------------------------------------------------------------
+constexpr int kIrSteps = 3;
+constexpr float kIrConv = 3e-4f;
+constexpr float kIrDiverge = 0.1f;
+
+// The implicit row's ratings and source factors (for the residual pass).
+struct IrArgs {
+  const int32_t* col;
+  const float* val;
+  const float* Y;
+  int64_t pb, pe;
+  float alpha;
 };
-template <>
-struct SmemBytes<8> {  // W1: transposition buffer (the Gram's 192-word staging fits in it)
+
+// LDS after the panel (floats): x in fp64 (natural order, 64) | batch weights g
+// (64 doubles) | their columns (64 ints) | residual rhs, correction (permuted, 16 NB).
+template <int CN>
+struct IrLds {
+  static constexpr int XS = PanelLds<CN>::SIZE, GS = XS + 128, CC = GS + 128, RV = CC + 64,
+                       DX = RV + 16 * CN, SIZE = DX + 16 * CN;
+  static_assert(XS % 4 == 0, "fp64 alignment");
+};
+
+// r_d = b_d - ((G + YtY + lambda n I) x)_d for an implicit row, lane d < k (fp64).
+// Batches of 64 ratings: lane j forms g_j = [r_j > 0](1 + c_j) - c_j (y_j . x), then
+// lane d accumulates sum_j g_j y_jd (coalesced row reads, L2-hot after the Gram pass).
+__device__ __forceinline__ double implicit_residual(const IrArgs& a, int ld, int k,
+                                                    const double* __restrict__ yty, double lam_n,
+                                                    const double* __restrict__ xs,
+                                                    double* __restrict__ gs, int* __restrict__ cc) {
+  const int lane = threadIdx.x & 63;
+  double r = 0.0;
+  for (int64_t base = a.pb; base < a.pe; base += 64) {
+    const int nb = (int)(a.pe - base < 64 ? a.pe - base : 64);
+    double g = 0.0;
+    int c = 0;
+    if (lane < nb) {
+      c = a.col[base + lane];
+      const double rv = (double)a.val[base + lane];
+      const float* y = a.Y + (int64_t)c * ld;
+      double s0 = 0.0, s1 = 0.0;
+      for (int d = 0; d < k; d += 4) {  // xs is zero past k (< ld, ld % 4 == 0)
+        const float4 v = *reinterpret_cast<const float4*>(y + d);
+        s0 = fma((double)v.x, xs[d], s0);
+        s1 = fma((double)v.y, xs[d + 1], s1);
+        s0 = fma((double)v.z, xs[d + 2], s0);
+        s1 = fma((double)v.w, xs[d + 3], s1);
+      }
+      const double c1 = (double)a.alpha * fabs(rv);
+      g = (rv > 0.0 ? 1.0 + c1 : 0.0) - c1 * (s0 + s1);
+    }
+    gs[lane] = g;
+    cc[lane] = c;
+    wave_lds_sync();
+    if (lane < k) {
+#pragma unroll 8
+      for (int j = 0; j < nb; ++j) r = fma(gs[j], (double)a.Y[(int64_t)cc[j] * ld + lane], r);
+    }
+    wave_lds_sync();
+  }
+  if (lane < k) {
+    for (int e = 0; e < k; ++e) {
+      const int hi = lane > e ? lane : e, lo = lane > e ? e : lane;
+      r = fma(-yty[hi * (hi + 1) / 2 + lo], xs[e], r);
+    }
+    r = fma(-lam_n, xs[lane], r);
+  }
+  return r;
+}
+
+// Refine the panel solution in Xv (permuted layout) in place; true once converged.
+template <int CN>
+__device__ __forceinline__ bool panel_refine(float* __restrict__ lds, const IrArgs& a, int ld,
+                                             int k, const double* __restrict__ yty,
+                                             double lam_n) {
+  typedef PanelLds<CN> Lo;
+  typedef IrLds<CN> Ir;
+  float* Xv = lds + Lo::X;
+  float* Zv = lds + Lo::Z;
+  const float* Dv = lds + Lo::D;
+  double* xs = reinterpret_cast<double*>(lds + Ir::XS);
+  double* gs = reinterpret_cast<double*>(lds + Ir::GS);
+  int* cc = reinterpret_cast<int*>(lds + Ir::CC);
+  float* Rv = lds + Ir::RV;
+  float* DX = lds + Ir::DX;
+  const int lane = threadIdx.x & 63;
+  const int pl = (lane % CN) * 16 + lane / CN;  // permuted slot of natural dim `lane`
+  bool conv = false;
+  for (int it = 0; it < kIrSteps; ++it) {
+    xs[lane] = lane < k ? (double)Xv[pl] : 0.0;  // k <= 64: one dim per lane
+    wave_lds_sync();
+    const double r = implicit_residual(a, ld, k, yty, lam_n, xs, gs, cc);
+    if (lane < 16 * CN) Rv[pl] = lane < k ? (float)r : 0.f;
+    wave_lds_sync();
+    block_fwd_subst<Lo::CS>(CN, lds + Lo::T, Rv, Zv);
+    block_back_subst<Lo::CS>(CN, lds + Lo::T, Zv, Dv, DX);
+    float nd = 0.f, nx = 0.f;
+    if (lane < 16 * CN) {
+      const float dx = DX[lane];
+      const float xn = Xv[lane] + dx;
+      Xv[lane] = xn;
+      nd = dx * dx;
+      nx = xn * xn;
+    }
+    wave_lds_sync();
+    for (int o = 32; o > 0; o >>= 1) {
+      nd += __shfl_xor(nd, o);
+      nx += __shfl_xor(nx, o);
+    }
+    if (nd <= (kIrConv * kIrConv) * nx) {
+      conv = true;
+      break;
+    }
+    if (!(nd <= (kIrDiverge * kIrDiverge) * nx)) break;  // (NaN included)
+  }
+  return conv;
+}
+
+template <int CN, bool IMPLICIT = false>
+struct SmemBytes {
+  static constexpr int value =
+      (int)sizeof(float) * (IMPLICIT ? IrLds<CN>::SIZE : PanelLds<CN>::SIZE);
+};
+template <bool IMPLICIT>
+struct SmemBytes<8, IMPLICIT> {  // W1: transposition buffer (the Gram's 192-word staging fits in it)
   static constexpr int value = (int)sizeof(float) * W1Lds::SIZE;
 };
 
@@ -1787,8 +1978,7 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
                                                  int64_t n_reg, unsigned char* smem, int k,
                                                  float reg, const double* __restrict__ yty,
                                                  float* __restrict__ xrow, int ld, int row,
-                                                 unsigned* __restrict__ rescue_cnt,
-                                                 int32_t* __restrict__ rescue_list) {
+                                                 RescueList rl, const IrArgs& ir) {
   constexpr int NT = Cfg<CN>::NT;
   float bq[CN];
   const int m = threadIdx.x & 15;
@@ -1823,8 +2013,17 @@ __device__ __forceinline__ void finish_and_solve(AccT (&tot)[Cfg<CN>::NT][4], Ac
     }
   }
   regularise_f32<CN>(A, (float)((double)reg * (double)n_reg), k);
-  const bool ok = panel_ldl_solve<CN>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
-  if (!ok) rescue_append(rescue_cnt, rescue_list, row);  // re-solved in fp64
+  float* lds = reinterpret_cast<float*>(smem);
+  if constexpr (IMPLICIT) {
+    // pivots checked here, accuracy a posteriori by the refinement
+    bool ok = panel_ldl_solve<CN, false, false>(A, bq, lds, k, xrow, ld);
+    if (ok) ok = panel_refine<CN>(lds, ir, ld, k, yty, (double)reg * (double)n_reg);
+    panel_store_x<CN>(lds + PanelLds<CN>::X, k, ok, xrow, ld);
+    if (!ok) rescue_append(rl, row);  // re-solved in fp64
+  } else {
+    const bool ok = panel_ldl_solve<CN>(A, bq, lds, k, xrow, ld);
+    if (!ok) rescue_append(rl, row);  // re-solved in fp64
+  }
 }
 
 // Partial-sum slot of one task: N tiles x 4 accumulator rows, NRA rhs values and
@@ -1911,8 +2110,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
-                                                    unsigned* __restrict__ rescue_cnt,
-                                                    int32_t* __restrict__ rescue_list);
+                                                    RescueList rl);
 
 // (k <= 64 keeps one gather step in flight: two steps need 187 registers, i.e. two
 // waves per SIMD instead of three, measured slower on configs[1]: 2.07 -> 2.24 ms/iter.)
@@ -1926,9 +2124,9 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const float* __restrict__ Y, float* __restrict__ X, int ld, int k, float reg, float alpha,
     const double* __restrict__ yty, float* __restrict__ slots, int32_t* __restrict__ status,
     const float* __restrict__ scal, const uint32_t* __restrict__ Ysp, int32_t kp,
-    int32_t zero_row, unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
+    int32_t zero_row, RescueList rl) {
   constexpr int NT = Cfg<CN>::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
   floatx4 acc[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -1968,7 +2166,7 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     rmax *= ldexpf(1.f, er);
     if (chunk < 0 && (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
                       rank_deficient_illcond<CN>(acc, inv2, pe - pb, k, reg))) {
-      rescue_append(rescue_cnt, rescue_list, row);
+      rescue_append(rl, row);
       return;
     }
   }
@@ -1990,10 +2188,11 @@ __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     // inverses + fp32 MFMA), in the Gram's scale
     static_assert(W1LdsT<4>::SIZE <= PanelLds<4>::SIZE, "W1<4> LDS");
     w1_finish_and_solve<false, 4, false>(acc, inv2, bt, n_reg, nullptr, smem, k, reg,
-                                  X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
+                                  X + (int64_t)row * ld, ld, row, rl);
   } else {
     finish_and_solve<CN, IMPLICIT, float>(tot, bt, n_reg, smem, k, reg, yty,
-                                          X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
+                                          X + (int64_t)row * ld, ld, row, rl,
+                                          IrArgs{col, val, Y, pb, pe, alpha});
   }
 }
 
@@ -2094,13 +2293,15 @@ __global__ __launch_bounds__(256) void heavy_sum_f64_kernel(const int32_t* __res
 
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
-    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
+    const float* __restrict__ val, const float* __restrict__ Y, float alpha,
+    const int32_t* __restrict__ heavy_rows,
     const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status, const float* __restrict__ scal,
-    unsigned* __restrict__ rescue_cnt, int32_t* __restrict__ rescue_list) {
+    RescueList rl) {
   constexpr int NT = Cfg<CN>::NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN, IMPLICIT>::value];
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
   double a64[NT][4], b64[CN];
@@ -2120,12 +2321,14 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
       for (int r = 0; r < 4; ++r)
         if (4 * q + r == m) d = fmaxf(d, (float)a64[tile_index(CN, c, c)][r] * s2);
     if (window_miss(d, (float)n_reg, (float)sl[(NT * 4 + CN) * 64 + lane])) {
-      rescue_append(rescue_cnt, rescue_list, row);
+      rescue_append(rl, row);
       return;
     }
   }
   finish_and_solve<CN, IMPLICIT, double>(a64, b64, n_reg, smem, k, reg, yty,
-                                         X + (int64_t)row * ld, ld, row, rescue_cnt, rescue_list);
+                                         X + (int64_t)row * ld, ld, row, rl,
+                                         IrArgs{col, val, Y, row_ptr[row], row_ptr[row + 1],
+                                                alpha});
 }
 
 // ---------------------------------------------------------------------------
@@ -2170,8 +2373,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
-                                                    unsigned* __restrict__ rescue_cnt,
-                                                    int32_t* __restrict__ rescue_list) {
+                                                    RescueList rl) {
   constexpr int NT_ = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   const float inv = 1.f / scale;  // power of two: exact
@@ -2212,7 +2414,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
     });
   }
   const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
-  if (!ok) rescue_append(rescue_cnt, rescue_list, row);  // re-solved in fp64
+  if (!ok) rescue_append(rl, row);  // re-solved in fp64
 }
 
 // Launch 1 (W1): heavy-row chunks (-> fp32 partial slots) and whole light rows
@@ -2225,8 +2427,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     int32_t n_chunks, int32_t n_light, const float* __restrict__ Y, float* __restrict__ X, int ld,
     int k, float reg, float alpha, const float* __restrict__ ytyC, float* __restrict__ slots,
     int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
-    int32_t kp, int32_t zero_row, unsigned* __restrict__ rescue_cnt,
-    int32_t* __restrict__ rescue_list) {
+    int32_t kp, int32_t zero_row, RescueList rl) {
   constexpr int CN = 8, NT = kW1NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
@@ -2274,7 +2475,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     rmax *= ldexpf(1.f, er);
     if (chunk < 0 && (window_miss(diag_max_lane<CN>(acc), (float)(pe - pb), rmax) ||
                       rank_deficient_illcond<CN>(acc, inv2, pe - pb, k, reg))) {
-      rescue_append(rescue_cnt, rescue_list, row);
+      rescue_append(rl, row);
       return;
     }
   }
@@ -2293,8 +2494,7 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
   w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
-                                               X + (int64_t)row * ld, ld, row, rescue_cnt,
-                                               rescue_list);
+                                               X + (int64_t)row * ld, ld, row, rl);
 }
 
 // ---------------------------------------------------------------------------
@@ -2346,8 +2546,7 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
                                          const float (&rj)[2], const uint32_t* __restrict__ Ysp,
                                          int ey, float reg, float* __restrict__ xrow, int ld,
                                          float* __restrict__ lds, int32_t* __restrict__ status,
-                                         unsigned* __restrict__ rescue_cnt,
-                                         int32_t* __restrict__ rescue_list) {
+                                         RescueList rl) {
   constexpr int NT = NB * (NB + 1) / 2;
   constexpr int NS = KP / 32;  // k-steps of 32 dims
   typedef FullTiles<NB> TS;
@@ -2404,7 +2603,7 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   });
   // split window guard: G_jj = |t_j|^2 <= KP max_d t_jd^2 (ratings are not split here)
   if (window_miss(diag_max_lane<NB>(acc), (float)KP, 0.f)) {
-    rescue_append(rescue_cnt, rescue_list, row);
+    rescue_append(rl, row);
     return;
   }
   // (2^2ey G + 2^2ey lambda n I) z = 2^2ey r; ratings j >= n: identity rows, rhs 0
@@ -2428,7 +2627,7 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
   for (int c = 0; c < NB; ++c) bcol[c] = rc[c] * inv;
   const bool ok = w1_solve_x<NB, false>(acc, bcol, lds, n, z);
   if (!ok) {  // re-solved in fp64 (the primal k x k system)
-    rescue_append(rescue_cnt, rescue_list, row);
+    rescue_append(rl, row);
     return;
   }
   // x = Y_S^T z: z split into f16 hi + lo after a power-of-two scale
@@ -2490,8 +2689,7 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const int32_t* __restrict__ rows, float* __restrict__ X, int ld,
     float reg, int32_t* __restrict__ status, const float* __restrict__ scal,
-    const uint32_t* __restrict__ Ysp, int32_t zero_row, unsigned* __restrict__ rescue_cnt,
-    int32_t* __restrict__ rescue_list) {
+    const uint32_t* __restrict__ Ysp, int32_t zero_row, RescueList rl) {
   static_assert(KP == 64 || KP == 128, "dual: k_pad 64 or 128");
   constexpr int NMAX = KP == 128 ? kDualMaxRatings : kDualMaxRatings64;
   __shared__ __attribute__((aligned(16))) float lds[W1LdsT<KP == 128 ? 6 : 2>::SIZE];
@@ -2515,17 +2713,14 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     rj[h] = j < n ? val[pb + j] : 0.f;
   }
   if constexpr (KP == 64) {
-    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt, rescue_list);
+    dual_row<2, 64>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rl);
   } else {
     if (n <= 32)
-      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
-                       rescue_list);
+      dual_row<2, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rl);
     else if (n <= 64)
-      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
-                       rescue_list);
+      dual_row<4, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rl);
     else
-      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rescue_cnt,
-                       rescue_list);
+      dual_row<6, 128>(row, n, cj, rj, Ysp, ey, reg, xrow, ld, lds, status, rl);
   }
 }
 
@@ -2578,8 +2773,7 @@ __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
     const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
     float* __restrict__ X, int ld, int k, float reg, int32_t* __restrict__ status,
-    const float* __restrict__ scal, unsigned* __restrict__ rescue_cnt,
-    int32_t* __restrict__ rescue_list) {
+    const float* __restrict__ scal, RescueList rl) {
   constexpr int CN = 8, NT = kW1NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
@@ -2597,12 +2791,12 @@ __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
   if constexpr (!IMPLICIT) {  // split window guard over the whole row (npos_f: max |rating|)
     const float s2 = ldexpf(1.f, 2 * split_exponent(scal[0]));
     if (window_miss(diag_max_lane<CN>(A) * s2, (float)n_reg, npos_f)) {
-      rescue_append(rescue_cnt, rescue_list, row);
+      rescue_append(rl, row);
       return;
     }
   }
   w1_finish_and_solve<false>(A, 1.f, bt, n_reg, nullptr, smem, k, reg, X + (int64_t)row * ld, ld,
-                             row, rescue_cnt, rescue_list);
+                             row, rl);
 }
 
 // Rescue launch: every row the fp32-grade path did not solve to the 1e-4 bar — its
@@ -2631,8 +2825,7 @@ __global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const float* __restrict__ Y, int ld, int k, float reg,
     float alpha, const double* __restrict__ yty, float* __restrict__ X,
-    int32_t* __restrict__ status, unsigned* __restrict__ rescue_cnt,
-    const int32_t* __restrict__ rescue_list) {
+    int32_t* __restrict__ status, RescueList rl) {
   constexpr int NPMAX = kMaxRank * (kMaxRank + 1) / 2;
   __shared__ double Ap[NPMAX];  // lower-packed A
   __shared__ double bs[kMaxRank];
@@ -2642,9 +2835,12 @@ __global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
   __shared__ int fail_s;
   const int tid = threadIdx.x;
   const int np = k * (k + 1) / 2;
-  const unsigned n_list = *rescue_cnt;
+  const unsigned n_app = *rl.cnt;
+  const unsigned n_list = n_app < rl.cap ? n_app : rl.cap;
+  if (n_app > rl.cap && blockIdx.x == 0 && tid == 0)
+    atomicExch(status, -1);  // appended past the list: the phases ran out of order
   for (unsigned it = blockIdx.x; it < n_list; it += gridDim.x) {
-    const int row = rescue_list[it];
+    const int row = rl.list[it];
     const int64_t pb = row_ptr[row], pe = row_ptr[row + 1];
     for (int e = tid; e < np; e += kRescueThreads) Ap[e] = IMPLICIT ? yty[e] : 0.0;
     for (int d = tid; d < k; d += kRescueThreads) bs[d] = 0.0;
@@ -2742,14 +2938,14 @@ __global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
     __syncthreads();  // LDS reused by the next listed row
   }
   // the list is consumed: the last block to finish (every block read the count before
-  // its increment) empties it for the next LAUNCH1 of this workspace.  rescue_cnt[1] is
+  // its increment) empties it for the next LAUNCH1 of this workspace.  rl.cnt[1] is
   // the finished-block counter (zeroed with the count by the prep, reset here).
   __syncthreads();
   if (tid == 0) {
     __threadfence();
-    if (atomicAdd(rescue_cnt + 1, 1u) == gridDim.x - 1) {
-      rescue_cnt[0] = 0u;
-      rescue_cnt[1] = 0u;
+    if (atomicAdd(rl.cnt + 1, 1u) == gridDim.x - 1) {
+      rl.cnt[0] = 0u;
+      rl.cnt[1] = 0u;
     }
   }
 }
@@ -2975,6 +3171,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
                                                     slot_bytes(k, n_chunks));
   unsigned* rescue_cnt = scal_u + 2;
+  const RescueList rl{rescue_cnt, rescue_list, (unsigned)(n_light + n_heavy)};
   // the rescue list (count at scale word 2, the rescue launch's finished-block counter
   // at word 3) starts empty at each Y prep (cleared by the prep's absmax launch: a fresh
   // workspace holds garbage) and is emptied by the RESCUE launch that consumes it, so the
@@ -3027,28 +3224,27 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                     chunk_begin, chunk_end, n_chunks,             \
                                                     n_light_primal, Y_src, X_dst, ld, k, reg,     \
                                                     alpha, yty_packed, slots_f, status_dev, scal,   \
-                                                    Ysp, kp, zero_row, rescue_cnt, rescue_list);  \
+                                                    Ysp, kp, zero_row, rl);  \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd && CN == 4 && !IMP) {                                                                  \
       gram_solve_dual_kernel<64><<<gd, 64, 0, st>>>(row_ptr, col, val,                            \
                                                     light_rows + n_light_primal, X_dst, ld, reg,  \
-                                                    status_dev, scal, Ysp, zero_row, rescue_cnt,  \
-                                                    rescue_list);                                 \
+                                                    status_dev, scal, Ysp, zero_row, rl);          \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_f64_kernel<Cfg<CN>::SLOT, IMP>                                                    \
           <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots_f);     \
       ALS_LAUNCH_CHECK();                                                                         \
-      reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,     \
+      reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, col, val, Y_src, alpha,            \
+                                                      heavy_rows, heavy_slot_begin,               \
                                                       slots_f, X_dst, ld, k, reg, yty_packed,     \
-                                                      status_dev, scal, rescue_cnt, rescue_list); \
+                                                      status_dev, scal, rl); \
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
     if (rescue) {                                                                                 \
       rescue64_kernel<IMP><<<kRescueGrid, kRescueThreads, 0, st>>>(                               \
-          row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rescue_cnt, \
-          rescue_list);                                                                           \
+          row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rl);        \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
   } while (0)
@@ -3060,13 +3256,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                                                    chunk_end, n_chunks, n_light_primal, Y_src,    \
                                                    X_dst, ld, k, reg, alpha, ytyC, slots_f,       \
                                                    status_dev, scal, Ysp, kp, zero_row,           \
-                                                   rescue_cnt, rescue_list);                      \
+                                                   rl);                      \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd) {                                                                                     \
       gram_solve_dual_kernel<128><<<gd, 64, 0, st>>>(row_ptr, col, val,                           \
                                                      light_rows + n_light_primal, X_dst, ld, reg, \
-                                                     status_dev, scal, Ysp, zero_row, rescue_cnt, \
-                                                     rescue_list);                                \
+                                                     status_dev, scal, Ysp, zero_row, rl);         \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
     if (g2) {                                                                                     \
@@ -3075,13 +3270,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_w1_kernel<IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,      \
                                                      slots_f, X_dst, ld, k, reg, status_dev,      \
-                                                     scal, rescue_cnt, rescue_list);              \
+                                                     scal, rl);              \
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \
     if (rescue) {                                                                                 \
       rescue64_kernel<IMP><<<kRescueGrid, kRescueThreads, 0, st>>>(                               \
-          row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rescue_cnt, \
-          rescue_list);                                                                           \
+          row_ptr, col, val, Y_src, ld, k, reg, alpha, yty_packed, X_dst, status_dev, rl);        \
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
   } while (0)

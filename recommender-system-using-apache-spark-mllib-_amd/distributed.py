@@ -457,9 +457,15 @@ class ShardedALS:
         self.half_sweep_users(reg, implicit, alpha)
 
     def check_status(self) -> None:
-        st = self.status.clone()
+        # (max, -min) over ranks: a failed row (> 0) and a rescue-list overflow (-1)
+        # both reach every rank
+        st = torch.cat([self.status, -self.status]).to(torch.int64)
         dist.all_reduce(st, op=dist.ReduceOp.MAX, group=self.group)
-        if int(st) != 0:
+        hi, neg = int(st[0]), int(st[1])
+        if neg > 0:
+            raise RuntimeError("als_solve_half rescue list overflow on some rank: the LAUNCH "
+                               "phases ran again before the RESCUE phase consumed the list")
+        if hi != 0:
             raise RuntimeError("Cholesky failed (non-positive pivot) on some rank: the normal "
                                "equations are not positive definite (Spark raises from dppsv)")
 

@@ -69,6 +69,9 @@ class Workspace:
         nbytes = max(int(nbytes), 256)
         if self.buf is None or self.buf.numel() < nbytes:
             self.buf = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            # the scale / rescue-count words: a call without PREP on a fresh buffer
+            # must not start from garbage
+            self.buf[:256].zero_()
             self.rating_scale_key = None
         if not keep_scale:
             self.rating_scale_key = None
@@ -290,6 +293,19 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
         ws.rating_scale_key = key
 
 
+def raise_status(s: int, where: str = "") -> None:
+    """Raise for a non-zero solve status word: row + 1 of a failed Cholesky (Spark's
+    dppsv info > 0), or -1 when the fp64 rescue list overflowed (als_solve_half's
+    LAUNCH phases ran twice without the RESCUE phase between them)."""
+    if s < 0:
+        raise RuntimeError(f"als_solve_half rescue list overflow{where}: the LAUNCH phases ran "
+                           "again before the RESCUE phase consumed the list (unsolved rows)")
+    if s > 0:
+        raise RuntimeError(
+            f"Cholesky failed (non-positive pivot) for dense row {s - 1}{where}: the normal "
+            "equations are not positive definite (Spark raises from LAPACK dppsv here)")
+
+
 # ---------------------------------------------------------------------------
 # K4/K5
 # ---------------------------------------------------------------------------
@@ -467,11 +483,7 @@ class ALSCore:
         self.half_sweep_users(reg, implicit, alpha)
 
     def check_status(self) -> None:
-        s = int(self.status.item())
-        if s != 0:
-            raise RuntimeError(
-                f"Cholesky failed (non-positive pivot) for dense row {s - 1}: the normal "
-                "equations are not positive definite (Spark raises from LAPACK dppsv here)")
+        raise_status(int(self.status.item()))
 
     def fit(self, rank, max_iter, reg, implicit=False, alpha=1.0, seed=0, U0=None,
             checkpoint_dir=None, checkpoint_interval=10, resume=False):

@@ -227,6 +227,7 @@ def resume_point_agreed(dirpath: Optional[str], resume, engine, rank: int, reg: 
     rank starts at the same iteration from the same state (or every rank raises)."""
     import torch
     import torch.distributed as dist
+    from .distributed import broadcast_capped
     if not resume or not dirpath:
         return 0, None, None
     fp = engine.fingerprint()  # collective: every rank
@@ -254,8 +255,7 @@ def resume_point_agreed(dirpath: Optional[str], resume, engine, rank: int, reg: 
     def bcast(F, n):
         t = (torch.as_tensor(F).to(device, torch.float32).contiguous() if proc == 0 else
              torch.empty((n, rank), dtype=torch.float32, device=device))
-        dist.broadcast(t, src=src, group=group)
-        return t
+        return broadcast_capped(t, src, "checkpoint factors", group)
 
     U = bcast(U, engine.n_users)
     V = bcast(V, engine.n_items) if has_v else None

@@ -129,6 +129,37 @@ def _guard(nbytes: int, what: str) -> None:
                            f"MAX_COLLECTIVE_BYTES = {MAX_COLLECTIVE_BYTES} (use more chunks)")
 
 
+def _capped_pieces(t: torch.Tensor, what: str):
+    """1-D views of the contiguous tensor t of at most MAX_COLLECTIVE_BYTES each (every
+    rank holds the same shape, so every rank issues the same calls)."""
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: collective on a non-contiguous tensor")
+    flat = t.view(-1)
+    per = max(1, MAX_COLLECTIVE_BYTES // t.element_size())
+    for s in range(0, flat.numel(), per):
+        piece = flat[s:s + per]
+        _guard(piece.numel() * piece.element_size(), what)
+        yield piece
+
+
+def all_reduce_capped(t: torch.Tensor, what: str, op=None, group=None) -> torch.Tensor:
+    """dist.all_reduce of t in place, split into calls of <= MAX_COLLECTIVE_BYTES (the
+    id-space flag and degree arrays of the setup grow with the id range: 2^31 ids would
+    be an 8 GiB int32 all_reduce in one call)."""
+    op = dist.ReduceOp.SUM if op is None else op
+    for piece in _capped_pieces(t, what):
+        dist.all_reduce(piece, op=op, group=group)
+    return t
+
+
+def broadcast_capped(t: torch.Tensor, src: int, what: str, group=None) -> torch.Tensor:
+    """dist.broadcast of t in place in calls of <= MAX_COLLECTIVE_BYTES (checkpointed
+    factor tables: 10M x 128 fp32 = 5.1 GB)."""
+    for piece in _capped_pieces(t, what):
+        dist.broadcast(piece, src=src, group=group)
+    return t
+
+
 def _ranges(deg: torch.Tensor, parts: int, cap_rows: Optional[int] = None):
     """Contiguous row ranges start[w] .. start[w+1], w < parts, balancing deg + ROW_WEIGHT
     (no row is split), with at most cap_rows rows per range (default ceil(PAD_CAP x
@@ -240,7 +271,7 @@ class ShardedALS:
         mm = torch.tensor([int(u.max()) if u.numel() else -big, int(i.max()) if i.numel() else -big,
                            -int(u.min()) if u.numel() else -big,
                            -int(i.min()) if i.numel() else -big], dtype=torch.int64, device=dev)
-        dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
+        all_reduce_capped(mm, "id range", dist.ReduceOp.MAX, group)
         (umax, imax), (umin, imin) = mm[:2].tolist(), (-mm[2:]).tolist()
         if umax < umin:
             raise ValueError("ALS needs at least one rating")
@@ -254,7 +285,7 @@ class ShardedALS:
         self.users = self._layout(u, u_space, uoff)
         self.items = self._layout(i, i_space, ioff)
         nz = torch.tensor([self.local_nnz], dtype=torch.int64, device=dev)
-        dist.all_reduce(nz, group=group)
+        all_reduce_capped(nz, "rating count", group=group)
         self.nnz = int(nz)
         # dense -> padded global numbering of both sides
         ud = self.users.dense_map[u.long()]
@@ -298,13 +329,13 @@ class ShardedALS:
         dev = self.device
         flag = torch.zeros(space, dtype=torch.int32, device=dev)
         flag[ids.long()] = 1
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        all_reduce_capped(flag, "id flags", dist.ReduceOp.MAX, self.group)
         present = torch.nonzero(flag).flatten().to(torch.int32)
         del flag
         dmap, uniq, n = self.K.index_build(present, space)
         deg = torch.zeros(n, dtype=torch.int64, device=dev)
         deg.index_add_(0, dmap[ids.long()].long(), torch.ones_like(ids, dtype=torch.int64))
-        dist.all_reduce(deg, group=self.group)
+        all_reduce_capped(deg, "row degrees", group=self.group)
         starts = _ranges(deg, self.world)
         degc = deg.cpu()
         # chunk ranges capped against the GLOBAL mean rows per (rank, chunk), so the
@@ -336,6 +367,7 @@ class ShardedALS:
         order = torch.argsort(dest, stable=True)
         send_counts = torch.bincount(dest, minlength=self.world).to(torch.int64)
         recv_counts = torch.empty_like(send_counts)
+        _guard(send_counts.numel() * send_counts.element_size(), "routing counts")
         dist.all_to_all_single(recv_counts, send_counts, group=self.group)
         sc, rc = send_counts.tolist(), recv_counts.tolist()
         out = []
@@ -355,7 +387,7 @@ class ShardedALS:
         per = max(1, MAX_COLLECTIVE_BYTES // (t.element_size() * W))
         rounds_t = torch.tensor([-(-max(max(sc), max(rc), 1) // per)], dtype=torch.int64,
                                 device=dev)
-        dist.all_reduce(rounds_t, op=dist.ReduceOp.MAX, group=self.group)
+        all_reduce_capped(rounds_t, "routing rounds", dist.ReduceOp.MAX, self.group)
         rounds = max(1, int(rounds_t.item()))
         if rounds == 1:
             dist.all_to_all_single(o, t, rc, sc, group=self.group)
@@ -422,7 +454,8 @@ class ShardedALS:
     def _yty(self, loc: torch.Tensor):
         # local rows of every chunk (padding rows are zero and add nothing), then all_reduce
         g = self.K.yty(loc.view(-1, loc.shape[-1]), loc.shape[0] * loc.shape[1], self.rank)
-        dist.all_reduce(g, group=self.group)
+        g = g.contiguous()
+        all_reduce_capped(g, "YtY", group=self.group)
         return g
 
     def _solve_and_gather(self, blocks, Y_full, X_loc, X_full, reg, implicit, alpha, yty):
@@ -460,7 +493,7 @@ class ShardedALS:
         # (max, -min) over ranks: a failed row (> 0) and a rescue-list overflow (-1)
         # both reach every rank
         st = torch.cat([self.status, -self.status]).to(torch.int64)
-        dist.all_reduce(st, op=dist.ReduceOp.MAX, group=self.group)
+        all_reduce_capped(st, "status", dist.ReduceOp.MAX, self.group)
         hi, neg = int(st[0]), int(st[1])
         if neg > 0:
             raise RuntimeError("als_solve_half rescue list overflow on some rank: the LAUNCH "
@@ -510,7 +543,7 @@ class ShardedALS:
         for blk in self.user_blocks:
             if blk is not None:
                 bits += self.K.block_values(blk).view(torch.int32).long().sum().to(self.device)
-        dist.all_reduce(bits, group=self.group)
+        all_reduce_capped(bits, "fingerprint", group=self.group)
         return {"nnz": int(self.nnz), "n_users": int(self.n_users), "n_items": int(self.n_items),
                 "rating_bits": int(bits), "item_id_sum": int(self.items.ids().long().sum())}
 
@@ -561,7 +594,7 @@ class ShardedALS:
         part = self.K.rmse_partial(us.keys(self._ids(users)), its.keys(self._ids(items)), r,
                                    us.padded_map(), its.padded_map(), self.U_full, self.V_full,
                                    self.rank).to(torch.float64)
-        dist.all_reduce(part, group=self.group)
+        all_reduce_capped(part, "rmse partial", group=self.group)
         sse, n = part.tolist()
         return (math.sqrt(sse / n) if n > 0 else float("nan")), int(n)
 

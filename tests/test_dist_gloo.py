@@ -222,31 +222,68 @@ def _route_worker(rank, world, port, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    # ids spread over a 20x wider space: the id-flag all_reduce of the setup covers
+    # 2,400 user ids (9.6 KB of int32) and must split under the small cap
     u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
+    u = u * 20
     sel = np.arange(len(u)) % world == rank
+    ck = os.path.join(out_dir, "ckpt_route")
     ref = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=2)
-    ref.fit(4, 2, 0.1, seed=3)
-    Dm.MAX_COLLECTIVE_BYTES = 64  # forces many routing rounds and many chunks
+    ref.fit(4, 2, 0.1, seed=3, checkpoint_dir=ck, checkpoint_interval=1)
+    ref_rmse = ref.rmse(u[sel], i[sel], r[sel])
+    # record the bytes of every collective call the package issues from here on
+    sizes = []
+    real = {n: getattr(dist, n) for n in ("all_reduce", "broadcast", "all_to_all_single",
+                                          "all_gather_into_tensor")}
+
+    def rec(name):
+        def f(*a, **kw):
+            ts = [x for x in a if isinstance(x, torch.Tensor)]
+            sizes.append((name, max(x.numel() * x.element_size() for x in ts)))
+            return real[name](*a, **kw)
+        return f
+    for n in real:
+        setattr(dist, n, rec(n))
+    Dm.MAX_COLLECTIVE_BYTES = 64  # forces many routing rounds, chunks and split reduces
     small = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
     ok = small.chunks >= 2
     for a, b in ((ref.user_blocks, small.user_blocks), (ref.item_blocks, small.item_blocks)):
         ok = ok and sum(x[0][-1] for x in a if x is not None) == \
             sum(x[0][-1] for x in b if x is not None)
     small.fit(4, 2, 0.1, U0_global=None, seed=3)  # every call within the 64-byte cap
+    small_rmse = small.rmse(u[sel], i[sel], r[sel])
+    # a resume broadcasts the checkpointed factor tables (split under the cap too)
+    res = Dm.ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels())
+    res.fit(4, 2, 0.1, seed=3, checkpoint_dir=ck, checkpoint_interval=0, resume=True)
+    for n, f in real.items():
+        setattr(dist, n, f)
     _, Ua = ref.user_factors()
     _, Ub = small.user_factors()
+    _, Ur = res.user_factors()
+    flags = [b for n, b in sizes if n == "all_reduce" and b == 64]
     np.save(os.path.join(out_dir, f"route_{rank}.npy"),
-            np.array([float(ok), float(np.abs(Ua.numpy() - Ub.numpy()).max())]))
+            np.array([float(ok), float(np.abs(Ua.numpy() - Ub.numpy()).max()),
+                      float(max(b for _, b in sizes)), float(len(sizes)),
+                      float(len(flags)), abs(ref_rmse[0] - small_rmse[0]),
+                      float(np.abs(Ua.numpy() - Ur.numpy()).max()),
+                      float(sum(1 for n, _ in sizes if n == "broadcast"))]))
     dist.destroy_process_group()
 
 
 def test_chunked_collectives_match(tmp_path):
-    """Routing in several all_to_all rounds and factor all-gathers in more chunks
-    (MAX_COLLECTIVE_BYTES lowered) give the same blocks and the same fit."""
+    """With MAX_COLLECTIVE_BYTES lowered to 64: routing in several all_to_all rounds,
+    factor all-gathers in more chunks, the setup's id-flag / degree all_reduces and a
+    resume's factor broadcast split into pieces — every collective call the package
+    issues (recorded at the torch.distributed functions) is within the cap, and the
+    blocks, the fit, the RMSE and the resumed factors equal the uncapped run's."""
     mp.spawn(_route_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     for w in range(2):
-        ok, diff = np.load(tmp_path / f"route_{w}.npy")
+        ok, diff, biggest, n_calls, n_full_reduces, drmse, dres, n_bcast = \
+            np.load(tmp_path / f"route_{w}.npy")
         assert ok == 1.0 and diff <= 1e-5
+        assert biggest <= 64 and n_calls > 0
+        assert n_full_reduces >= 2  # the flag / degree arrays went out in 64-byte pieces
+        assert drmse <= 1e-9 and dres == 0.0 and n_bcast > 1
 
 
 def _resume_worker(rank, world, port, out_dir, mode):

@@ -34,3 +34,45 @@ def test_no_unguarded_dpp_hazards(tmp_path):
         found = isa_hazards.scan(out.read_text().split("\n"))
         bad += [(src,) + f for f in found]
     assert not bad, bad[:10]
+
+
+def test_scanner_follows_labels_and_branches():
+    """The scanner's window runs through fall-through labels and conditional branches
+    and seeds each branch target with the branching block's pending writes (the case a
+    per-basic-block reset misses); an unconditional branch ends the fall-through path."""
+    import isa_hazards
+    asm = """
+kern:
+  v_mov_b32 v4, v1
+.LBB0_1:
+  v_fmac_f32_dpp v8, v4, v9 row_newbcast:1
+  s_endpgm
+kern2:
+  v_mov_b32 v5, v1
+  s_cbranch_scc1 .LBB1_2
+  s_nop 7
+  s_nop 7
+.LBB1_2:
+  v_fmac_f32_dpp v8, v5, v9 row_newbcast:1
+  s_endpgm
+kern3:
+  v_mov_b32 v6, v1
+  s_branch .LBB2_9
+.LBB2_3:
+  v_fmac_f32_dpp v8, v6, v9 row_newbcast:1
+  s_endpgm
+.LBB2_9:
+  s_nop 1
+  s_branch .LBB2_3
+kern4:
+  v_mov_b32 v7, v1
+  s_nop 1
+  v_fmac_f32_dpp v8, v7, v9 row_newbcast:1
+  s_endpgm
+""".split("\n")
+    found = isa_hazards.scan(asm)
+    fns = sorted({f[0] for f in found})
+    # kern: through a fall-through label; kern2: the branch's target skips the nops;
+    # kern3: the write reaches the read through two unconditional branches but with
+    # the s_nop 1 + branch wait states on that path (>= 2): clean; kern4: guarded
+    assert fns == ["kern", "kern2"], found

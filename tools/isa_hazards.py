@@ -10,8 +10,12 @@ Rule checked (MI355X_MICROARCH / CDNA3 ISA hazard table, conservatively):
   * VALU write of VGPR v -> DPP or permlane read of v: >= 2 wait states between them;
   * MFMA write of v -> VALU read of v through DPP / permlane: >= 11 wait states for the
     16x16 shapes (at most 8 passes), >= 19 for 32x32 (16 passes).
-Wait states = intervening instructions (1 each) + s_nop N (N + 1).  Straight-line code
-only: the window restarts at labels and branches, which hold their own waits.
+Wait states = intervening instructions (1 each) + s_nop N (N + 1).  The window follows
+the control flow: it runs on through labels (a label adds no wait states) and
+conditional branches (one wait state each, fall-through path), and each label starts
+from the merge (worst case) of its fall-through window and the windows of every branch
+that targets it, iterated to a fixed point over back edges.  Only an unconditional
+s_branch / s_setpc ends the fall-through window.
 
     python tools/isa_hazards.py file.s        (exit 1 and a listing when any is found)
 """
@@ -40,51 +44,88 @@ def _is_dpp_read(op: str, ins: str) -> bool:
     return "row_newbcast" in ins or "permlane" in op or "_dpp" in op
 
 
+_LABEL = re.compile(r"^([_A-Za-z.$][\w.$]*):")
+_WINDOW = 24
+
+
+def _merge(a, b):
+    """Worst case of two windows: every pending write of either, newest last."""
+    out = sorted(set(a) | set(b), key=lambda e: -e[4])
+    return out[-_WINDOW:]
+
+
+def _scan_once(insns, entry, found):
+    """One pass over the instructions with the label entry windows `entry` (label ->
+    window); returns the windows each branch carries to its target."""
+    carried = {}
+    fn = None
+    win = []  # (op, dst regs frozenset, is_mfma, is_valu, wait states since) newest last
+    reach = True  # the current point is reached by fall-through
+    for kind, a, b in insns:
+        if kind == "label":
+            if not a.startswith(".L"):
+                fn, win = a, []
+            win = _merge(win if reach else [], entry.get(a, []))
+            reach = True
+            continue
+        op, ins, args = a, b, None
+        args = _split(ins)[1]
+        if op.startswith("s_cbranch") or op == "s_branch" or op.startswith("s_setpc"):
+            tgt = args[0] if args else None
+            if tgt is not None and tgt.startswith(".L"):
+                carried[tgt] = _merge(carried.get(tgt, []), win)
+            if op.startswith("s_cbranch"):
+                win = [(o, d, m, v, w + 1) for (o, d, m, v, w) in win]
+            else:
+                win, reach = [], False
+            continue
+        if op == "s_nop":
+            n = int(args[0], 0) + 1 if args else 1
+            win = [(o, d, m, v, w + n) for (o, d, m, v, w) in win]
+            continue
+        if op.startswith("v_") and _is_dpp_read(op, ins):
+            srcs = set()
+            for x in args[1:]:
+                srcs |= _regs(x)
+            if "permlane" in op or op.startswith("v_fmac"):
+                srcs |= _regs(args[0])  # tied / swapped operand is read too
+            for (wop, dst, mfma, valu, w) in win:
+                need = (19 if "32x32" in wop else 11) if mfma else (2 if valu else 0)
+                if dst & srcs and w < need:
+                    found.add((fn, wop, ins, w))
+        dst = frozenset(_regs(args[0])) if args and op.startswith("v_") else frozenset()
+        mfma = "mfma" in op
+        valu = op.startswith("v_") and not mfma and not op.startswith(("v_readlane", "v_readfirstlane"))
+        win = [(o, d, m, v, w + 1) for (o, d, m, v, w) in win]
+        win.append((op, dst, mfma, valu, 0))
+        win = win[-_WINDOW:]
+    return carried
+
+
 def scan(lines):
     """-> [(function, writer, reader, wait_states)] of hazardous pairs."""
-    found = []
-    fn = None
-    recent = []  # (op, dst regs, is_mfma, is_valu) of the straight-line window, newest last
-    waits_since = []  # wait states elapsed after each entry of `recent`
+    insns = []
     for raw in lines:
         line = raw.split(";")[0].rstrip()
         if not line.strip():
             continue
-        if re.match(r"^[_A-Za-z.$][\w.$]*:", line):
-            if not line.startswith(".L"):
-                fn = line.split(":")[0]
-            recent, waits_since = [], []
+        m = _LABEL.match(line)
+        if m:
+            insns.append(("label", m.group(1), None))
             continue
         ins = line.strip()
         if ins.startswith("."):
             continue
-        op, args = _split(ins)
-        if op.startswith("s_cbranch") or op == "s_branch" or op.startswith("s_setpc"):
-            recent, waits_since = [], []
-            continue
-        if op == "s_nop":
-            n = int(args[0], 0) + 1 if args else 1
-            waits_since = [w + n for w in waits_since]
-            continue
-        if op.startswith("v_") and _is_dpp_read(op, ins):
-            srcs = set()
-            for a in args[1:]:
-                srcs |= _regs(a)
-            if "permlane" in op or op.startswith("v_fmac"):
-                srcs |= _regs(args[0])  # tied / swapped operand is read too
-            for (wop, dst, mfma, valu), w in zip(recent, waits_since):
-                need = (19 if "32x32" in wop else 11) if mfma else (2 if valu else 0)
-                if dst & srcs and w < need:
-                    found.append((fn, wop, ins, w))
-        dst = _regs(args[0]) if args and op.startswith("v_") else set()
-        mfma = "mfma" in op
-        valu = op.startswith("v_") and not mfma and not op.startswith(("v_readlane", "v_readfirstlane"))
-        waits_since = [w + 1 for w in waits_since]
-        recent.append((op, dst, mfma, valu))
-        waits_since.append(0)
-        if len(recent) > 24:
-            recent, waits_since = recent[-24:], waits_since[-24:]
-    return found
+        insns.append(("ins", _split(ins)[0], ins))
+    entry = {}
+    found = set()
+    for _ in range(4):  # back edges: iterate the label entry windows to a fixed point
+        found = set()
+        carried = _scan_once(insns, entry, found)
+        if carried == entry:
+            break
+        entry = carried
+    return sorted(found, key=lambda f: (str(f[0]), f[2]))
 
 
 def main():

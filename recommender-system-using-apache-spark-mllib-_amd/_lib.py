@@ -18,8 +18,24 @@ import threading
 import torch  # noqa: F401  (must precede the CDLL load; see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# ALS_HIP_LIB: an alternative build of the same ABI (dev A/B runs)
-LIB_PATH = os.environ.get("ALS_HIP_LIB") or os.path.join(_HERE, "libals_hip.so")
+PRODUCT_LIB = os.path.join(_HERE, "libals_hip.so")
+
+
+def _lib_path() -> str:
+    """The in-tree product library.  ALS_HIP_LIB (another build of the same ABI, for
+    dev A/B runs under tools/) is honoured only together with ALS_HIP_DEV=1, so a
+    stray environment variable can never swap the library the product loads."""
+    alt = os.environ.get("ALS_HIP_LIB")
+    if alt and os.environ.get("ALS_HIP_DEV") == "1":
+        return alt
+    if alt:
+        import warnings
+        warnings.warn("ALS_HIP_LIB is ignored without ALS_HIP_DEV=1 (dev A/B builds only); "
+                      f"loading {PRODUCT_LIB}")
+    return PRODUCT_LIB
+
+
+LIB_PATH = _lib_path()
 _lib = None
 _lock = threading.Lock()
 

@@ -102,6 +102,14 @@ def save(dirpath: str, iteration: int, rank: int, reg: float, implicit: bool, al
     """Write the state after `iteration` completed iterations (a new generation, then
     the atomic commit of als_state.json, then removal of the older generations)."""
     os.makedirs(dirpath, exist_ok=True)
+    # the layout this commit replaces: a format-1 checkpoint kept its arrays next to
+    # the JSON, and only then are same-named top-level files ours to remove
+    prev_format = None
+    try:
+        with open(os.path.join(dirpath, STATE)) as f:
+            prev_format = json.load(f).get("format")
+    except (OSError, ValueError, AttributeError):
+        pass
     gen = f"{_GEN}{int(iteration):06d}-{uuid.uuid4().hex[:8]}"
     tmp = os.path.join(dirpath, "." + gen + ".tmp")
     os.makedirs(tmp)
@@ -133,11 +141,12 @@ def save(dirpath: str, iteration: int, rank: int, reg: float, implicit: bool, al
         if name != gen and (name.startswith(_GEN) or (name.startswith("." + _GEN)
                                                        and name.endswith(".tmp"))):
             shutil.rmtree(os.path.join(dirpath, name), ignore_errors=True)
-    for name in (IDS, FACTORS, IIDS, IFACTORS):  # a format-1 layout's top-level files
-        try:
-            os.remove(os.path.join(dirpath, name))
-        except FileNotFoundError:
-            pass
+    if prev_format == 1:  # the replaced format-1 layout's top-level arrays
+        for name in (IDS, FACTORS, IIDS, IFACTORS):
+            try:
+                os.remove(os.path.join(dirpath, name))
+            except FileNotFoundError:
+                pass
 
 
 def load(dirpath: str) -> Optional[State]:

@@ -490,18 +490,12 @@ __device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
   return tk_min_u64(x, tk_partner64<32>(x));
 }
 
-// MODE (dev ablation only, tools/dev_topk.hip; the product launches MODE 0):
-// 1 = exact scores only (no filter), 2 = coarse filter against an unbeatable
-// threshold (no refinement, no insertions, no early exit), 3 = as 0 but each wave
-// writes its count of blocks past the coarse filter to score_out[wave] and of
-// tiles swept to score_out[waves + wave] instead of the lists; 4 = 2 without the V
-// stream (the first tiles re-staged: compute / LDS only).
 // Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
 // rows), 4 with LDS lists (top > 128: the lists of 64 RG rows fill the LDS).
 // (Quad lists with two row groups, one wavefront per SIMD, measured round 4 at
 // configs[4]'s 262,144-user sample: top-100 390 ms vs 233 ms with one group.)
 __host__ __device__ constexpr int tk_nw(int topr) { return topr > 0 ? 8 : 4; }
-template <int NK, int RG, int TOPR, int MODE = 0>
+template <int NK, int RG, int TOPR>
 __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const float* __restrict__ Q, int64_t n_q,
                                                          const uint4* __restrict__ Vsp,
                                                          const uint4* __restrict__ Vlo,
@@ -617,7 +611,6 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   float nv_pre[DEPTH], nv_cur = 0.f;
   auto fetch = [&](int64_t vb, auto dc) {
     constexpr int D = decltype(dc)::value;
-    if (MODE == 4 && vb > 2 * VT) return;  // dev: no V stream (stale tiles re-staged)
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const int x = threadIdx.x + NT * e;
@@ -662,12 +655,10 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   auto refine = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG]) {
     const int64_t vr = ibase + m < n_v ? ibase + m : n_v - 1;  // rows past n_v: NaN anyway
     uint4* scr = loscr + w * NK * 64;
-    if constexpr (MODE != 5) {  // dev MODE 5: stale lo halves, no DMA wait (timing only)
 #pragma unroll
-      for (int s = 0; s < NK; ++s)
-        __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    for (int s = 0; s < NK; ++s)
+      __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
       const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
@@ -692,18 +683,10 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
         ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? fmaf(-s4[r], nvt, t4[r]) : __builtin_inff();
     }
   };
-  float sink = 0.f;
-  int n_offer = 0, n_tiles = 0;
   // acc: hi.hi scores of the block (refined in place when it passes the coarse
   // filter); tbr: the block's B rows in the tile
   auto filter = [&](floatx4 (&acc)[RG], int64_t ibase, const int* bperm, const uint4* tbr) {
     // acc[g][r] = scaled score(row GR g + 16w + 4q + r, V row ibase + m)
-    if constexpr (MODE == 1) {
-      refine(tbr, ibase, acc);
-#pragma unroll
-      for (int g = 0; g < RG; ++g) sink += fmaxf(fmaxf(acc[g][0], acc[g][1]), fmaxf(acc[g][2], acc[g][3]));
-      return;
-    }
     if constexpr (TOPR > 0) {
       // coarse: hi.hi >= the coarse threshold; then the exact scores go to the
       // owners against the same threshold (a weaker test than the k-th score: the
@@ -716,7 +699,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
 #pragma unroll
         for (int g = 0; g < RG; ++g)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= (MODE == 2 || MODE == 4 ? 3.0e38f : ts[g][r]);
+          for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= ts[g][r];
         if (__ballot(c) == 0) return;
       }
       refine(tbr, ibase, acc);
@@ -725,7 +708,6 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       for (int g = 0; g < RG; ++g)
 #pragma unroll
         for (int r = 0; r < 4; ++r) pr[g][r] = !fullw || acc[g][r] >= ts[g][r];
-      if constexpr (MODE == 3) ++n_offer;
       float* st = sblk + w * RG * 256;  // [g][item m][row]
       uint64_t b[RG][4];
 #pragma unroll
@@ -825,7 +807,6 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
                                acc[g][2] >= ts[g][2] || acc[g][3] >= ts[g][3]);
         hit = __ballot(p) != 0;
       }
-      if constexpr (MODE == 3) n_offer += hit ? 1 : 0;
       if (hit)
         topk_offer(acc[g], (int)ibase, n_v, bperm, ts[g], ti[g], lk, len, GR * g + 16 * w,
                    top, live[g]);
@@ -855,7 +836,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       // tile on can reach: k-th > (|q| + 1)(NV + 1)(1 + 2^-7) (dead rows: +inf)
       bool open = false;
       if constexpr (TOPR > 0) {
-        if (MODE != 1) refresh();
+        refresh();
 #pragma unroll
         for (int g = 0; g < RG; ++g) {
           const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
@@ -872,11 +853,11 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
           for (int r = 0; r < 4; ++r) open = open || !(ts[g][r] > (0x1p9f + 4.f) * s4[r] * nvt);
         }
       }
-      const bool wdone = (MODE == 0 || MODE == 3) && __ballot(open) == 0;
+      const bool wdone = __ballot(open) == 0;
       if (!wdone) {
-        if constexpr (MODE == 3) ++n_tiles;
         floatx4 acc0[RG], acc1[RG];
-        if constexpr (TOPR > 0 && MODE == 0) {
+        if constexpr (TOPR > 0) {
+          static_assert(NC % 4 == 0, "quartets of 16-row blocks per tile");
           // four blocks scored back to back, then one ballot for all four against the
           // current coarse thresholds (they only rise, so a quartet with no pair past
           // them has none past the later ones): the LDS -> MFMA -> compare -> branch
@@ -939,11 +920,6 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       if (!tile_step(vb, D1{})) break;
       vb += VT;
     }
-  }
-  if constexpr (MODE != 0) {
-    if (lane == 0) score_out[blockIdx.x * NW + w] = MODE == 1 ? sink : (float)n_offer;
-    if (MODE == 3 && lane == 0) score_out[(gridDim.x + blockIdx.x) * NW + w] = (float)n_tiles;
-    return;
   }
   if constexpr (QUAD) {
     // output position of a real entry = number of real entries above it in the

@@ -147,3 +147,19 @@ def test_product_never_imports_the_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in re.sub(r'""".*?"""|#.*', "", src, flags=re.S), f
+
+
+def test_library_override_needs_the_dev_flag(tmp_path):
+    """ALS_HIP_LIB alone cannot swap the product library (only with ALS_HIP_DEV=1)."""
+    import subprocess
+    import sys
+    code = ("import _pkgload; _pkgload.load(); from als_mi355x import _lib; "
+            "print(_lib.LIB_PATH == _lib.PRODUCT_LIB)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = {k: v for k, v in os.environ.items() if k not in ("ALS_HIP_LIB", "ALS_HIP_DEV")}
+    for extra, want in (({"ALS_HIP_LIB": str(tmp_path / "x.so")}, "True"),
+                        ({"ALS_HIP_LIB": str(tmp_path / "x.so"), "ALS_HIP_DEV": "1"}, "False")):
+        p = subprocess.run([sys.executable, "-W", "ignore", "-c", code], cwd=root,
+                           env=dict(base, **extra), capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-2000:]
+        assert p.stdout.strip().splitlines()[-1] == want

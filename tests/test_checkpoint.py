@@ -205,3 +205,18 @@ def test_gpu_ml_fit_resumes_from_checkpoint_dir(tmp_path):
     m = ALS(rank=8, maxIter=6, regParam=0.1, seed=1, checkpointInterval=3).setCheckpointDir(d).fit(df)
     assert torch.equal(m.engine.U, ref.engine.U) and torch.equal(m.engine.V, ref.engine.V)
     assert C.load(d).iteration == 6
+
+
+def test_save_keeps_user_files_that_share_the_format1_names(tmp_path):
+    """Same-named .npy files the user keeps in the checkpoint directory are not ours
+    unless a format-1 checkpoint is being replaced: a save into a fresh directory (and
+    over a format-2 checkpoint) leaves them alone."""
+    e = _eng()
+    d = tmp_path / "ck"
+    d.mkdir()
+    mine = np.arange(7, dtype=np.int32)
+    np.save(d / C.FACTORS, mine, allow_pickle=False)
+    C.maybe_save(str(d), 1, 1, e, 3, 0.1, False, 1.0, init=C.init_key(1, None))
+    C.maybe_save(str(d), 1, 2, e, 3, 0.1, False, 1.0, init=C.init_key(1, None))
+    np.testing.assert_array_equal(np.load(d / C.FACTORS), mine)
+    assert C.load(str(d)).iteration == 2

@@ -1,6 +1,6 @@
 """Dev A/B timing of half-sweep variants (NOT the bench): one workload, the library
 named by ALS_HIP_LIB (a tools/ab/build_solve.sh build) or the product one.
-    ALS_HIP_LIB=tools/ab/libals_x.so python tools/ab_solve.py c1|c2|c3 [steps]
+    ALS_HIP_DEV=1 ALS_HIP_LIB=tools/ab/libals_x.so python tools/ab_solve.py c1|c2|c3 [steps]
 Prints one JSON line: ms per iteration and the event time of each phase launch."""
 import json
 import os

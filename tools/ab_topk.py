@@ -1,6 +1,6 @@
 """Dev A/B timing of recommendForAll variants (NOT the bench): the configs[3] factors
 after two ALS iterations (10M users x 1M items, rank 128), top-10 and top-100 for a
-262,144-user prefix (or all users with --all), with the library named by ALS_HIP_LIB (a
+262,144-user prefix (or all users with --all), with the library named by ALS_HIP_LIB (+ ALS_HIP_DEV=1; a
 tools/ab/build_solve.sh build) or the product one; a 64-user sample is checked against
 the fp64 oracle (identical except fp64 ties within 1e-5).
     ALS_HIP_LIB=tools/ab/libals_x.so python tools/ab_topk.py [--all]"""

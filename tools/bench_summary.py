@@ -9,7 +9,7 @@ import sys
 def main():
     d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
     r = d["roofline"]
-    print(f"value {d['value']:.4g} ms/step {d['ms_per_step']:.4f} frac {r['frac']:.4f} "
+    print(f"value {d['value']:.4g} ms/step {d['ms_per_step']:.4f} {r.get('bound')} frac {r['frac']:.4f} "
           f"launch_us {r['avg_launch_us']:.1f} limiter {r.get('limiter')} "
           f"dram_frac {r.get('counter_dram_frac')}")
     if d.get("dual"):
@@ -34,7 +34,11 @@ def main():
                     kern.replace(" ", "") in name.replace(" ", ""):
                 avg_ns = float(row.get("AverageNs") or row.get("Average") or 0)
                 calls = int(row.get("Calls") or 0)
-                frac = r["algorithmic_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9 / 8000.0
+                if r.get("bound") == "mfma":  # fp32-grade algorithmic flops vs 157.3 TF
+                    fl = r["fp32_grade_view"]["algorithmic_flops_per_launch"]
+                    frac = fl / (avg_ns * 1e-9) / 1e12 / 157.3
+                else:
+                    frac = r["algorithmic_bytes_per_launch"] / (avg_ns * 1e-9) / 1e9 / 8000.0
                 print(f"rocprof {name[:60]} calls {calls} avg_us {avg_ns / 1e3:.1f} "
                       f"recomputed frac {frac:.4f} vs line {r['frac']:.4f} "
                       f"(2 launches/step = {2 * avg_ns / 1e6:.4f} ms vs ms_per_step "

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-3 profiles of the bench workloads, one `bench.py --only W` run per pass:
+# Profiles of the bench workloads, one `bench.py --only W` run per pass:
 # a --kernel-trace --stats run and four --pmc passes (counter sets below, each
 # within the gfx950 per-pass limits), folded per workload into
-# gpurun_out/pmc_r03/pmc_summary.json (tools/pmc_fold.py, format 2).
-# Usage: bash tools/gpu_pmc_r03.sh c1 c2 c3 c4     (any subset)
+# gpurun_out/pmc_run/pmc_summary.json (tools/pmc_fold.py, format 2).
+# Usage: bash tools/gpu_pmc_run.sh c1 c2 c3 c4     (any subset)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp
 ROOT=${GRAFT_REPO_ROOT:-/root/repo}
-OUT=$ROOT/gpurun_out/pmc_r03
+OUT=$ROOT/gpurun_out/pmc_run
 mkdir -p $OUT
 [ -f $ROOT/profiles/pmc_summary.json ] && [ ! -f $OUT/pmc_summary.json ] && cp $ROOT/profiles/pmc_summary.json $OUT/pmc_summary.json
 PA="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_BUSY_CYCLES"

@@ -1,5 +1,5 @@
 """Dev: configs[4] top-10 / top-100 timing on configs[3]-shaped factors (2 ALS
-iterations from the seed), for the library ALS_HIP_LIB points at.
+iterations from the seed), for the library ALS_HIP_LIB points at (with ALS_HIP_DEV=1).
     python tools/topk_big.py [sample]"""
 import os
 import sys
@@ -27,33 +27,6 @@ def main():
     torch.cuda.synchronize()
     Q = core.U[:s].contiguous()
     lib = os.environ.get("ALS_HIP_LIB", "default")
-    if "--count" in sys.argv:  # offers per wave (tools/libals_topk_dev.so, MODE 3)
-        import ctypes
-        from als_mi355x import _lib
-        L = ctypes.CDLL(os.path.join(ROOT, "tools", "libals_topk_dev.so"))
-        P, I64 = ctypes.c_void_p, ctypes.c_int64
-        L.dev_topk.argtypes = [ctypes.c_int, P, I64, P, I64, ctypes.c_int, ctypes.c_int,
-                               ctypes.c_int, P, P, P, ctypes.c_size_t, P, P]
-        n_v = core.n_items
-        for top in (10, 100):
-            ws = torch.empty(int(_lib.lib().als_topk_workspace_bytes(s, n_v, 128, top)),
-                             dtype=torch.uint8, device=dev)
-            idx = torch.empty((s, top), dtype=torch.int32, device=dev)
-            sc = torch.empty((s, top), dtype=torch.float32, device=dev)
-            dbg = torch.zeros(s * 4 + 64, dtype=torch.float32, device=dev)
-            st = torch.cuda.current_stream().cuda_stream
-            for mode in (0, 3):
-                rc = L.dev_topk(mode, Q.data_ptr(), s, core.V.data_ptr(), n_v, Q.shape[1], 128, top,
-                                idx.data_ptr(), sc.data_ptr(), ws.data_ptr(), ws.numel(),
-                                dbg.data_ptr(), st)
-                assert rc == 0, rc
-            torch.cuda.synchronize()
-            rg = 2 if top <= 16 else 1
-            waves = (s + 64 * rg - 1) // (64 * rg) * 4
-            cnt = dbg[:waves].double()
-            blocks = (n_v + 15) // 16 * rg
-            print(f"top{top}: offers/wave mean {float(cnt.mean()):.0f} max {float(cnt.max()):.0f} "
-                  f"of {blocks} blocks", flush=True)
     for top in (10, 100):
         E.topk_rows(Q, s, core.V, core.n_items, 128, top)
         torch.cuda.synchronize()

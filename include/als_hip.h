@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ALS_ABI_VERSION 5
+#define ALS_ABI_VERSION 6
 
 #define ALS_OK 0
 #define ALS_EINVAL (-1)   /* bad argument (shape, null pointer, rank) */
@@ -134,7 +134,17 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * system (push-through identity (Y^T Y + lambda n I)^-1 Y^T r =
  * Y^T (Y Y^T + lambda n I)^-1 r), allowed for explicit feedback, 32 < k <= 128,
  * reg > 0 only (a longer row there is reported through status_dev).
- * n_light_primal = n_light keeps every row on the primal path. */
+ * n_light_primal = n_light keeps every row on the primal path.
+ * Two-segment schedules (ABI 6; the sharded engine's pipelined item half-sweep,
+ * distributed.py): chunk task c of this call writes partial slot chunk_slot0 + c,
+ * and heavy_slot_begin2 (nullable, n_heavy + 1 entries) gives each heavy row a
+ * second slot range, summed with the first in LAUNCH2.  A half-sweep whose source
+ * rows arrive in two parts then runs as two calls on one workspace: the early
+ * segments' chunk partials (PREP over the arrived prefix of Y_src, LAUNCH1,
+ * chunk_slot0 = 0), then the late segments' (chunk_slot0 = number of early slots)
+ * with LAUNCH2 and RESCUE over every row; the workspace is sized for all slots
+ * (the slot region sits before the split table, so the two calls' different n_src
+ * leave the early partials in place).  Normal calls pass NULL and 0. */
 #define ALS_PHASE_LAUNCH1 1
 #define ALS_PHASE_LAUNCH2 2
 #define ALS_PHASE_PREP 4
@@ -148,7 +158,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* light_rows, int32_t n_light, int32_t n_light_primal,
                    const int32_t* heavy_rows, const int32_t* heavy_slot_begin, int32_t n_heavy,
                    const int32_t* chunk_row, const int64_t* chunk_begin, const int64_t* chunk_end,
-                   int32_t n_chunks,
+                   int32_t n_chunks, const int32_t* heavy_slot_begin2, int32_t chunk_slot0,
                    const float* Y_src, int64_t n_src, float* X_dst, int32_t ld, int32_t k,
                    float reg, int implicit, float alpha, const double* yty_packed,
                    int32_t* status_dev, void* ws, size_t ws_bytes, int phases, void* stream);

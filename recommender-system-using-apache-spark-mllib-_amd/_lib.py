@@ -58,8 +58,9 @@ SIGNATURES = {
     "als_schedule_count": (ctypes.c_int, [P, I32, I32, P, P]),
     "als_schedule_build": (ctypes.c_int, [P, I32, I32, I32, I32, I32, P, P, P, P, P, P, P, SZ, P]),
     "als_solve_workspace_bytes": (SZ, [I32, I32, I64, I32]),
-    "als_solve_half": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, I32, P, P, P, I32, P, I64, P, I32,
-                                      I32, F32, ctypes.c_int, F32, P, P, P, SZ, ctypes.c_int, P]),
+    "als_solve_half": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, I32, P, P, P, I32, P, I32, P, I64,
+                                      P, I32, I32, F32, ctypes.c_int, F32, P, P, P, SZ,
+                                      ctypes.c_int, P]),
     "als_k_pad": (I32, [I32]),
     "als_yty_workspace_bytes": (SZ, [I64, I32]),
     "als_yty": (ctypes.c_int, [P, I64, I32, I32, P, P, SZ, P]),
@@ -71,7 +72,7 @@ SIGNATURES = {
     "als_topk": (ctypes.c_int, [P, I64, P, I64, I32, I32, I32, P, P, P, SZ, P]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class ALSNativeError(RuntimeError):

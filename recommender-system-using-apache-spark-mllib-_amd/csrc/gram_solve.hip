@@ -2265,38 +2265,60 @@ __global__ __launch_bounds__(256) void absmax_kernel(const float* __restrict__ x
 // thread per slot element, four interleaved partial sums in a fixed order), rounded
 // once to fp32 into its first slot; each thread reads and writes only its own element.
 // Explicit: the last 64 entries (each chunk's scaled max |rating|) take the max.
+// The partial slots of heavy row h: [slot_begin[h], slot_begin[h+1]) and, for a
+// two-segment schedule (slot_begin2 != null: the sharded engine's pipelined item
+// side, whose rows have an early and a late rating segment), [slot_begin2[h],
+// slot_begin2[h+1]).  The first slot of the union is the row's home slot, where
+// launch 2a leaves the sum.
+struct SlotRange {
+  int s0, n1, t0, n;
+  __device__ __forceinline__ int at(int i) const { return i < n1 ? s0 + i : t0 + (i - n1); }
+  __device__ __forceinline__ int home() const { return at(0); }
+};
+__device__ __forceinline__ SlotRange slot_range(const int32_t* __restrict__ sb,
+                                                const int32_t* __restrict__ sb2, int h) {
+  SlotRange r;
+  r.s0 = sb[h];
+  r.n1 = sb[h + 1] - r.s0;
+  r.t0 = sb2 ? sb2[h] : 0;
+  r.n = r.n1 + (sb2 ? sb2[h + 1] - r.t0 : 0);
+  return r;
+}
+
 template <int SLOT, bool IMPLICIT>
 __global__ __launch_bounds__(256) void heavy_sum_f64_kernel(const int32_t* __restrict__ slot_begin,
+                                                            const int32_t* __restrict__ slot_begin2,
                                                             float* __restrict__ slots) {
   const int h = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= SLOT) return;
-  const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
-  if (s1 - s0 <= 1) return;
+  const SlotRange sr = slot_range(slot_begin, slot_begin2, h);
+  if (sr.n <= 1) return;
+  const int64_t home = (int64_t)sr.home() * SLOT + e;
   if (!IMPLICIT && e >= SLOT - 64) {
     float mx = 0.f;
-    for (int s = s0; s < s1; ++s) mx = fmaxf(mx, slots[(int64_t)s * SLOT + e]);
-    slots[(int64_t)s0 * SLOT + e] = mx;
+    for (int i = 0; i < sr.n; ++i) mx = fmaxf(mx, slots[(int64_t)sr.at(i) * SLOT + e]);
+    slots[home] = mx;
     return;
   }
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    a0 += (double)slots[(int64_t)s * SLOT + e];
-    a1 += (double)slots[(int64_t)(s + 1) * SLOT + e];
-    a2 += (double)slots[(int64_t)(s + 2) * SLOT + e];
-    a3 += (double)slots[(int64_t)(s + 3) * SLOT + e];
+  int i = 0;
+  for (; i + 4 <= sr.n; i += 4) {
+    a0 += (double)slots[(int64_t)sr.at(i) * SLOT + e];
+    a1 += (double)slots[(int64_t)sr.at(i + 1) * SLOT + e];
+    a2 += (double)slots[(int64_t)sr.at(i + 2) * SLOT + e];
+    a3 += (double)slots[(int64_t)sr.at(i + 3) * SLOT + e];
   }
-  for (; s < s1; ++s) a0 += (double)slots[(int64_t)s * SLOT + e];
-  slots[(int64_t)s0 * SLOT + e] = (float)((a0 + a1) + (a2 + a3));
+  for (; i < sr.n; ++i) a0 += (double)slots[(int64_t)sr.at(i) * SLOT + e];
+  slots[home] = (float)((a0 + a1) + (a2 + a3));
 }
 
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
     const float* __restrict__ val, const float* __restrict__ Y, float alpha,
-    const int32_t* __restrict__ heavy_rows,
-    const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
+    const int32_t* __restrict__ heavy_rows, const int32_t* __restrict__ slot_begin,
+    const int32_t* __restrict__ slot_begin2, const float* __restrict__ slots,
     float* __restrict__ X, int ld, int k, float reg, const double* __restrict__ yty,
     int32_t* __restrict__ status, const float* __restrict__ scal,
     RescueList rl) {
@@ -2307,8 +2329,9 @@ __global__ __launch_bounds__(64, 2) void reduce_solve_kernel(
   double a64[NT][4], b64[CN];
   zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
-  // the row's chunk slots were summed into its first slot (heavy_sum_f64_kernel)
-  const float* sl = slots + (int64_t)slot_begin[h] * Cfg<CN>::SLOT;
+  // the row's chunk slots were summed into its home slot (heavy_sum_f64_kernel)
+  const float* sl =
+      slots + (int64_t)slot_range(slot_begin, slot_begin2, h).home() * Cfg<CN>::SLOT;
   add_slot_f32<NT, CN>(sl, a64, b64, npos);
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (row_ptr[row + 1] - row_ptr[row]);
   if constexpr (!IMPLICIT) {  // split window guard over the whole row
@@ -2734,27 +2757,28 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
 // slot (each thread reads and writes only its own element: in place is safe).
 template <bool IMPLICIT>
 __global__ __launch_bounds__(256) void heavy_sum_w1_kernel(const int32_t* __restrict__ slot_begin,
+                                                           const int32_t* __restrict__ slot_begin2,
                                                            float* __restrict__ slots,
                                                            const double* __restrict__ yty) {
   constexpr int CN = 8, NT = kW1NT, NE = (NT * 4 + CN + 1) * 64;
   const int h = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= NE) return;
-  const int s0 = slot_begin[h], s1 = slot_begin[h + 1];
+  const SlotRange sr = slot_range(slot_begin, slot_begin2, h);
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  int s = s0;
-  for (; s + 4 <= s1; s += 4) {
-    a0 += (double)slots[(int64_t)s * kW1Slot + e];
-    a1 += (double)slots[(int64_t)(s + 1) * kW1Slot + e];
-    a2 += (double)slots[(int64_t)(s + 2) * kW1Slot + e];
-    a3 += (double)slots[(int64_t)(s + 3) * kW1Slot + e];
+  int i = 0;
+  for (; i + 4 <= sr.n; i += 4) {
+    a0 += (double)slots[(int64_t)sr.at(i) * kW1Slot + e];
+    a1 += (double)slots[(int64_t)sr.at(i + 1) * kW1Slot + e];
+    a2 += (double)slots[(int64_t)sr.at(i + 2) * kW1Slot + e];
+    a3 += (double)slots[(int64_t)sr.at(i + 3) * kW1Slot + e];
   }
-  for (; s < s1; ++s) a0 += (double)slots[(int64_t)s * kW1Slot + e];
+  for (; i < sr.n; ++i) a0 += (double)slots[(int64_t)sr.at(i) * kW1Slot + e];
   double v = (a0 + a1) + (a2 + a3);
   const int ent = e >> 6;
   if (!IMPLICIT && ent == NT * 4 + CN) {  // the chunks' scaled max |rating|: max, not sum
     float mx = 0.f;
-    for (s = s0; s < s1; ++s) mx = fmaxf(mx, slots[(int64_t)s * kW1Slot + e]);
+    for (i = 0; i < sr.n; ++i) mx = fmaxf(mx, slots[(int64_t)sr.at(i) * kW1Slot + e]);
     v = mx;
   }
   if (IMPLICIT && ent < NT * 4) {
@@ -2764,22 +2788,23 @@ __global__ __launch_bounds__(256) void heavy_sum_w1_kernel(const int32_t* __rest
     const int hi = i > j ? i : j, lo = i > j ? j : i;
     v += yty[hi * (hi + 1) / 2 + lo];
   }
-  slots[(int64_t)s0 * kW1Slot + e] = (float)v;
+  slots[(int64_t)sr.home() * kW1Slot + e] = (float)v;
 }
 
 // Launch 2b: one wavefront per heavy row solves from its summed slot.
 template <bool IMPLICIT>
 __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ heavy_rows,
-    const int32_t* __restrict__ slot_begin, const float* __restrict__ slots,
-    float* __restrict__ X, int ld, int k, float reg, int32_t* __restrict__ status,
-    const float* __restrict__ scal, RescueList rl) {
+    const int32_t* __restrict__ slot_begin, const int32_t* __restrict__ slot_begin2,
+    const float* __restrict__ slots, float* __restrict__ X, int ld, int k, float reg,
+    int32_t* __restrict__ status, const float* __restrict__ scal, RescueList rl) {
   constexpr int CN = 8, NT = kW1NT;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
   const int h = blockIdx.x;
   const int row = heavy_rows[h];
-  const float* sl = slots + (int64_t)slot_begin[h] * kW1Slot + lane;
+  const float* sl =
+      slots + (int64_t)slot_range(slot_begin, slot_begin2, h).home() * kW1Slot + lane;
   floatx4 A[NT];
   float bt[CN];
 #pragma unroll
@@ -3116,12 +3141,14 @@ static size_t slot_bytes(int32_t k, int32_t n_chunks) {
 }
 
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows) {
-  // 256 B of scale words (max |Y_src|, max |rating|, rescue count) | split table
-  // ((n_src + 1) x k_pad words, explicit) | partial slots of the heavy-row chunks |
-  // rescue list (n_rows).  The first two sit at fixed offsets, so calls over blocks
-  // that share Y_src can share one prep (phases).
-  return 256 + ytyc_bytes(k) + solve_table_bytes(k, n_src) + slot_bytes(k, n_chunks) +
-         align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0));
+  // 256 B of scale words (max |Y_src|, max |rating|, rescue count) | C-layout YtY
+  // (W1 implicit) | partial slots of the heavy-row chunks (n_chunks, counted from
+  // slot 0: chunk_slot0 + the call's chunks) | rescue list (n_rows) | split table
+  // ((n_src + 1) x k_pad words, explicit).  The slots sit at a fixed offset, so the
+  // two calls of a two-segment half-sweep (different n_src) share them.
+  return 256 + ytyc_bytes(k) + slot_bytes(k, n_chunks) +
+         align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0)) +
+         solve_table_bytes(k, n_src);
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -3129,6 +3156,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
                    const int32_t* heavy_rows,
                    const int32_t* heavy_slot_begin, int32_t n_heavy, const int32_t* chunk_row,
                    const int64_t* chunk_begin, const int64_t* chunk_end, int32_t n_chunks,
+                   const int32_t* heavy_slot_begin2, int32_t chunk_slot0,
                    const float* Y_src, int64_t n_src, float* X_dst, int32_t ld, int32_t k,
                    float reg, int implicit, float alpha, const double* yty_packed,
                    int32_t* status_dev, void* ws, size_t ws_bytes, int phases, void* stream) {
@@ -3153,9 +3181,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   ALS_REQUIRE(n_src >= 0 && n_src < (int64_t(1) << 31), ALS_EINVAL,
               "als_solve_half: n_src %lld not in [0, 2^31)", (long long)n_src);
   const int32_t n_rows = n_light + n_heavy;
-  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_chunks, n_src, n_rows), ALS_EWORKSPACE,
+  ALS_REQUIRE(chunk_slot0 >= 0 && (int64_t)chunk_slot0 + n_chunks < (int64_t(1) << 31),
+              ALS_EINVAL, "als_solve_half: chunk_slot0 %d out of range", chunk_slot0);
+  const int32_t n_slots = chunk_slot0 + n_chunks;  // slot region: [0, n_slots)
+  ALS_REQUIRE(ws_bytes >= als_solve_workspace_bytes(k, n_slots, n_src, n_rows), ALS_EWORKSPACE,
               "als_solve_half: workspace %zu < %zu", ws_bytes,
-              als_solve_workspace_bytes(k, n_chunks, n_src, n_rows));
+              als_solve_workspace_bytes(k, n_slots, n_src, n_rows));
   ALS_REQUIRE(phases >= 1 && phases <= ALS_PHASE_ALL, ALS_EINVAL,
               "als_solve_half: phases must be in [1, %d]", ALS_PHASE_ALL);
   ALS_REQUIRE((reinterpret_cast<uintptr_t>(ws) & 15) == 0, ALS_EINVAL,
@@ -3165,11 +3196,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   unsigned* scal_u = static_cast<unsigned*>(ws);
   const float* scal = reinterpret_cast<const float*>(scal_u);
   float* ytyC = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
-  uint32_t* Ysp = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k));
-  double* slots = reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k) +
-                                            solve_table_bytes(k, n_src));
+  double* slots = reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k));
   int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
-                                                    slot_bytes(k, n_chunks));
+                                                    slot_bytes(k, n_slots));
+  uint32_t* Ysp = reinterpret_cast<uint32_t*>(
+      reinterpret_cast<char*>(rescue_list) +
+      align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0)));
   unsigned* rescue_cnt = scal_u + 2;
   const RescueList rl{rescue_cnt, rescue_list, (unsigned)(n_light + n_heavy)};
   // the rescue list (count at scale word 2, the rescue launch's finished-block counter
@@ -3223,7 +3255,9 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       gram_solve_kernel<CN, IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_row,     \
                                                     chunk_begin, chunk_end, n_chunks,             \
                                                     n_light_primal, Y_src, X_dst, ld, k, reg,     \
-                                                    alpha, yty_packed, slots_f, status_dev, scal,   \
+                                                    alpha, yty_packed,                            \
+                                                    slots_f + (size_t)chunk_slot0 * Cfg<CN>::SLOT, \
+                                                    status_dev, scal,                             \
                                                     Ysp, kp, zero_row, rl);  \
     ALS_LAUNCH_CHECK();                                                                           \
     if (gd && CN == 4 && !IMP) {                                                                  \
@@ -3234,10 +3268,12 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_f64_kernel<Cfg<CN>::SLOT, IMP>                                                    \
-          <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin, slots_f);     \
+          <<<dim3((Cfg<CN>::SLOT + 255) / 256, g2), 256, 0, st>>>(heavy_slot_begin,               \
+                                                                  heavy_slot_begin2, slots_f);     \
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_kernel<CN, IMP><<<g2, 64, 0, st>>>(row_ptr, col, val, Y_src, alpha,            \
                                                       heavy_rows, heavy_slot_begin,               \
+                                                      heavy_slot_begin2,                          \
                                                       slots_f, X_dst, ld, k, reg, yty_packed,     \
                                                       status_dev, scal, rl); \
     }                                                                                             \
@@ -3254,7 +3290,8 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     if (g1)                                                                                       \
       gram_solve_w1_kernel<IMP><<<g1, 64, 0, st>>>(row_ptr, col, val, light_rows, chunk_begin,    \
                                                    chunk_end, n_chunks, n_light_primal, Y_src,    \
-                                                   X_dst, ld, k, reg, alpha, ytyC, slots_f,       \
+                                                   X_dst, ld, k, reg, alpha, ytyC,                \
+                                                   slots_f + (size_t)chunk_slot0 * kW1Slot,       \
                                                    status_dev, scal, Ysp, kp, zero_row,           \
                                                    rl);                      \
     ALS_LAUNCH_CHECK();                                                                           \
@@ -3266,10 +3303,11 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
     }                                                                                             \
     if (g2) {                                                                                     \
       heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot + 255) / 256, g2), 256, 0, st>>>(                 \
-          heavy_slot_begin, slots_f, yty_packed);                                                 \
+          heavy_slot_begin, heavy_slot_begin2, slots_f, yty_packed);                              \
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_w1_kernel<IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,      \
-                                                     slots_f, X_dst, ld, k, reg, status_dev,      \
+                                                     heavy_slot_begin2, slots_f, X_dst, ld, k,    \
+                                                     reg, status_dev,                             \
                                                      scal, rl);              \
     }                                                                                             \
     ALS_LAUNCH_CHECK();                                                                           \

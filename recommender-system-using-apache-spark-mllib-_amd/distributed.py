@@ -57,6 +57,7 @@ class HipKernels:
         self.chunk = chunk or E.DEFAULT_CHUNK
         self.max_chunks = 0  # heavy-row chunks of the largest block: one workspace layout
         self.max_rows = 0    # rows of the largest block (rescue list)
+        self.split_ws = {}   # per-block workspaces of the pipelined (two-segment) item side
 
     def index_build(self, ids: torch.Tensor, id_space: int):
         idx = self.E.build_index(ids.to(self.device, torch.int32).contiguous(), id_space, self.ws)
@@ -84,6 +85,18 @@ class HipKernels:
         E.solve_half(block, Y, X, rank, reg, implicit, alpha, yty, status, self.ws,
                      phases=E.PHASE_ALL if first else E.PHASE_ALL & ~E.PHASE_PREP,
                      ws_chunks=self.max_chunks, ws_rows=self.max_rows)
+
+    def split_schedule(self, block, seg, n_src_early: int):
+        """Two-segment schedule of an item block (pipelined item half-sweep)."""
+        return self.E.split_schedule(block, seg, n_src_early, self.chunk)
+
+    def solve_split(self, block, sched, part, Y, X, rank, reg, implicit, alpha, yty, status,
+                    key):
+        """One part ("early" / "late") of a two-segment half-sweep; `key` names the block's
+        own workspace (its early partials must stay in place until its late call)."""
+        ws = self.split_ws.setdefault(key, self.E.Workspace(self.device))
+        self.E.solve_half_split(block, sched, part, Y, X, rank, reg, implicit, alpha, yty,
+                                status, ws)
 
     def predict(self, u_keys, i_keys, umap, imap, U, V, rank) -> torch.Tensor:
         E = self.E
@@ -248,7 +261,7 @@ class ShardedALS:
     """ALS with users and items sharded over the ranks of `group`."""
 
     def __init__(self, users, items, ratings, device=None, group=None, kernels=None,
-                 chunks: Optional[int] = None):
+                 chunks: Optional[int] = None, pipeline: Optional[bool] = None):
         self.group = group
         self.proc = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -297,7 +310,18 @@ class ShardedALS:
         self.user_blocks = self._blocks(self.users, ru, rc, rv, self.items)
         ri_, rc_, rv_ = self._route(self.items.owner_of(idn), i_pad, u_pad, r)
         self.item_rows = self._local_rows(self.items)
-        self.item_blocks = self._blocks(self.items, ri_, rc_, rv_, self.users)
+        # pipelined item half-sweep (default with several ranks and >= 2 user chunks):
+        # each item row's ratings are split into the users of chunks 0..C-2 (early) and
+        # of chunk C-1 (late), so the early partial normal equations are formed while
+        # the last user chunk's all-gather is still in flight (_pipelined_items)
+        if pipeline is None:
+            pipeline = self.world > 1
+        self.pipeline = bool(pipeline) and self.users.chunks >= 2
+        self.item_split = None
+        self.item_blocks = self._blocks(self.items, ri_, rc_, rv_, self.users,
+                                        split=self.pipeline)
+        self._pending_u = []  # async all-gathers of U chunks not yet waited for
+        self._yty_u = None    # YtY of the final U (implicit, pipelined): formed early
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
         self.rank = 0  # factor rank (k); the process rank is self.proc
         self._dense_cache = {}
@@ -349,9 +373,21 @@ class ShardedALS:
     def _local_rows(self, side: SideLayout) -> int:
         return int(side.starts[self.proc + 1] - side.starts[self.proc])
 
-    def _blocks(self, side: SideLayout, rows_pad, cols_pad, vals, other: SideLayout):
-        """Per-chunk rating blocks of this rank's rows (rows_pad: padded positions)."""
+    def _blocks(self, side: SideLayout, rows_pad, cols_pad, vals, other: SideLayout,
+                split: bool = False):
+        """Per-chunk rating blocks of this rank's rows (rows_pad: padded positions).
+        split: order every row's ratings early-first — columns (padded rows of `other`)
+        in its chunks 0..C-2, then those in its last chunk (the CSR build is stable) —
+        and keep each block's two-segment schedule in self.item_split."""
         W, rpc = self.world, side.rows_per_chunk
+        late = None
+        if split:
+            late = (cols_pad.long() // (W * other.rows_per_chunk)) == other.chunks - 1
+            order = torch.argsort(late.to(torch.int8), stable=True)
+            rows_pad, cols_pad, vals, late = rows_pad[order], cols_pad[order], vals[order], \
+                late[order]
+            self.item_split = []
+        n_src_early = (other.chunks - 1) * W * other.rows_per_chunk
         p = rows_pad.long()
         c = p // (W * rpc)
         j = (p % rpc).to(torch.int32)
@@ -359,9 +395,21 @@ class ShardedALS:
         for cc in range(side.chunks):
             n_c = side.chunk_rows(self.proc, cc)
             sel = c == cc
-            out.append(self.K.build_block(j[sel], cols_pad[sel], vals[sel], n_c,
-                                          W * other.rows_per_rank) if n_c > 0 else None)
+            blk = self.K.build_block(j[sel], cols_pad[sel], vals[sel], n_c,
+                                     W * other.rows_per_rank) if n_c > 0 else None
+            out.append(blk)
+            if split:
+                sched = None
+                if blk is not None:
+                    ne = torch.bincount(j[sel & ~late].long(), minlength=n_c)
+                    seg = self._row_starts(blk, n_c) + ne.to(torch.int64)
+                    sched = self.K.split_schedule(blk, seg, n_src_early)
+                self.item_split.append(sched)
         return out
+
+    def _row_starts(self, blk, n_rows: int) -> torch.Tensor:
+        rp = blk.row_ptr if hasattr(blk, "row_ptr") else torch.as_tensor(blk[0])
+        return rp[:n_rows].to(self.device, torch.int64)
 
     def _route(self, dest: torch.Tensor, a: torch.Tensor, b: torch.Tensor, v: torch.Tensor):
         order = torch.argsort(dest, stable=True)
@@ -420,6 +468,8 @@ class ShardedALS:
         all global dense user rows (unit-norm Gaussian rows from `seed`), sliced to
         this rank's rows; U0 / U0_global: an explicit [n_users_dense, rank] start."""
         U0 = U0 if U0 is not None else U0_global
+        self._drain()
+        self._yty_u = None
         self.rank = rank
         self._dense_cache = {}
         ld = self.K.ld(rank)
@@ -458,8 +508,11 @@ class ShardedALS:
         all_reduce_capped(g, "YtY", group=self.group)
         return g
 
-    def _solve_and_gather(self, blocks, Y_full, X_loc, X_full, reg, implicit, alpha, yty):
-        """Solve chunk c, start its all-gather, go on with chunk c+1; wait at the end."""
+    def _solve_and_gather(self, blocks, Y_full, X_loc, X_full, reg, implicit, alpha, yty,
+                          before_last=None, wait=True):
+        """Solve chunk c, start its all-gather, go on with chunk c+1; wait at the end
+        (wait=False: return the pending all-gathers).  before_last runs after the last
+        chunk's solve, before its all-gather is issued."""
         Xf = X_full.view(X_loc.shape[0], -1, X_full.shape[1])
         _guard(Xf[0].numel() * Xf.element_size(), "factor all_gather")
         works = []
@@ -469,27 +522,84 @@ class ShardedALS:
                 self.K.solve_half(blk, Y_full, X_loc[c], self.rank, reg, implicit, alpha, yty,
                                   self.status, first=first)
                 first = False
+            if before_last is not None and c == len(blocks) - 1:
+                before_last()
             works.append(dist.all_gather_into_tensor(Xf[c], X_loc[c], group=self.group,
+                                                     async_op=True))
+        self._dense_cache = {}
+        if not wait:
+            return works
+        for w in works:
+            w.wait()
+        return []
+
+    def _drain(self) -> None:
+        """Wait for the U all-gathers a pipelined user half-sweep left in flight."""
+        for w in self._pending_u:
+            w.wait()
+        self._pending_u = []
+
+    def _pipelined_items(self, reg, implicit, alpha, yty):
+        """Item half-sweep over the two-segment schedules: the early partials of every
+        item chunk (ratings of users in U chunks 0..C-2) are formed while U chunk C-1's
+        all-gather is still in flight; then, once it has arrived, the late partials, the
+        per-row fp64 sums and the solves, each chunk's V all-gather issued behind it."""
+        pend = self._pending_u
+        for w in pend[:-1]:
+            w.wait()
+        for c, blk in enumerate(self.item_blocks):
+            if blk is not None:
+                self.K.solve_split(blk, self.item_split[c], "early", self.U_full, self.V_loc[c],
+                                   self.rank, reg, implicit, alpha, yty, self.status, ("i", c))
+        for w in pend[-1:]:
+            w.wait()
+        self._pending_u = []
+        Vf = self.V_full.view(self.V_loc.shape[0], -1, self.V_full.shape[1])
+        _guard(Vf[0].numel() * Vf.element_size(), "factor all_gather")
+        works = []
+        for c, blk in enumerate(self.item_blocks):
+            if blk is not None:
+                self.K.solve_split(blk, self.item_split[c], "late", self.U_full, self.V_loc[c],
+                                   self.rank, reg, implicit, alpha, yty, self.status, ("i", c))
+            works.append(dist.all_gather_into_tensor(Vf[c], self.V_loc[c], group=self.group,
                                                      async_op=True))
         for w in works:
             w.wait()
         self._dense_cache = {}
 
     def half_sweep_items(self, reg, implicit=False, alpha=1.0):
-        yty = self._yty(self.U_loc) if implicit else None
+        if implicit:
+            yty = self._yty_u if self._yty_u is not None else self._yty(self.U_loc)
+        else:
+            yty = None
+        self._yty_u = None
+        if self.pipeline:
+            self._pipelined_items(reg, implicit, alpha, yty)
+            return
+        self._drain()
         self._solve_and_gather(self.item_blocks, self.U_full, self.V_loc, self.V_full, reg,
                                implicit, alpha, yty)
 
     def half_sweep_users(self, reg, implicit=False, alpha=1.0):
+        self._drain()
         yty = self._yty(self.V_loc) if implicit else None
-        self._solve_and_gather(self.user_blocks, self.V_full, self.U_loc, self.U_full, reg,
-                               implicit, alpha, yty)
+        before_last = None
+        if self.pipeline and implicit:
+            # the next item half-sweep's YtY of the final U: its all_reduce is issued
+            # before U chunk C-1's all-gather, so the early item partials need not wait
+            # for that gather
+            def before_last():
+                self._yty_u = self._yty(self.U_loc)
+        self._pending_u = self._solve_and_gather(
+            self.user_blocks, self.V_full, self.U_loc, self.U_full, reg, implicit, alpha, yty,
+            before_last=before_last, wait=not self.pipeline)
 
     def iterate(self, reg, implicit=False, alpha=1.0):
         self.half_sweep_items(reg, implicit, alpha)
         self.half_sweep_users(reg, implicit, alpha)
 
     def check_status(self) -> None:
+        self._drain()
         # (max, -min) over ranks: a failed row (> 0) and a rescue-list overflow (-1)
         # both reach every rank
         st = torch.cat([self.status, -self.status]).to(torch.int64)
@@ -529,6 +639,7 @@ class ShardedALS:
     def _set_dense(self, user_side: bool, F) -> None:
         """Overwrite one replicated factor table (and this rank's rows) from a dense
         [n, rank] host/device array (every rank passes the same array)."""
+        self._drain()
         side, full, loc = (self.users, self.U_full, self.U_loc) if user_side else \
             (self.items, self.V_full, self.V_loc)
         F = torch.as_tensor(F).to(self.device, torch.float32)
@@ -567,6 +678,7 @@ class ShardedALS:
     def _dense(self, user_side: bool, cache: bool = True) -> torch.Tensor:
         """Dense-order copy [n, ld] of one replicated factor table (cached per fit state
         unless cache=False)."""
+        self._drain()
         if user_side in self._dense_cache:
             return self._dense_cache[user_side]
         side, full = (self.users, self.U_full) if user_side else (self.items, self.V_full)
@@ -581,6 +693,7 @@ class ShardedALS:
 
     def predict(self, users, items) -> torch.Tensor:
         """fp64 <u, v> of this rank's pairs (NaN for unknown ids); no collective."""
+        self._drain()
         us, its = self.users, self.items
         return self.K.predict(us.keys(self._ids(users)), its.keys(self._ids(items)),
                               us.padded_map(), its.padded_map(), self.U_full, self.V_full,
@@ -589,6 +702,7 @@ class ShardedALS:
     def rmse(self, users, items, ratings):
         """computeError over the pairs of ALL ranks: local fused (sse, n), then an
         all_reduce (RecommenderSystem.py:123 reduce, :126 count)."""
+        self._drain()
         us, its = self.users, self.items
         r = torch.as_tensor(ratings).to(self.device, torch.float32)
         part = self.K.rmse_partial(us.keys(self._ids(users)), its.keys(self._ids(items)), r,

@@ -284,13 +284,97 @@ def solve_half(block: RatingBlock, Y: torch.Tensor, X: torch.Tensor, rank: int, 
                            ptr(block.light_rows), block.n_light, n_primal,
                            ptr(block.heavy_rows),
                            ptr(block.heavy_slot_begin), block.n_heavy, ptr(block.chunk_row),
-                           ptr(block.chunk_begin), ptr(block.chunk_end), block.n_chunks,
+                           ptr(block.chunk_begin), ptr(block.chunk_end), block.n_chunks, 0, 0,
                            ptr(Y), Y.shape[0], ptr(X), X.shape[1], rank, float(reg),
                            int(bool(implicit)),
                            float(alpha), ptr(yty), ptr(status), ptr(w), w.numel(), int(phases),
                            stream_ptr(X.device)), "als_solve_half")
     if (phases & PHASE_RSCALE) and ws.shared_rating_scale:
         ws.rating_scale_key = key
+
+
+@dataclass
+class SplitSchedule:
+    """Two-segment schedule of one CSR block (ABI 6, the sharded engine's pipelined item
+    half-sweep).  Row r's ratings are [row_ptr[r], seg[r]) — the early segment, whose
+    source rows lie in the first n_src_early rows of Y (already gathered) — then
+    [seg[r], row_ptr[r+1]) (the late segment: the source chunk still arriving).  Each
+    segment is cut into <= chunk-rating tasks; every row goes through the heavy-row
+    path (fp32 task partials summed per row in fp64, then solved), early slots first."""
+    n_src_early: int
+    rows: torch.Tensor          # int32 [n]: every row of the block, ascending
+    slot_begin: torch.Tensor    # int32 [n+1]: early slots of row r
+    slot_begin2: torch.Tensor   # int32 [n+1]: late slots of row r (after all early ones)
+    early: tuple                # (chunk_row, chunk_begin, chunk_end, n_tasks)
+    late: tuple
+
+    @property
+    def n_slots(self) -> int:
+        return self.early[3] + self.late[3]
+
+
+def _segment_tasks(row_ids, begin, end, chunk: int, dev):
+    """<= chunk-rating tasks over the per-row ranges [begin[r], end[r])."""
+    ln = (end - begin).clamp(min=0)
+    cnt = (ln + chunk - 1) // chunk
+    n = int(cnt.sum())
+    slot_begin = torch.zeros(len(ln) + 1, dtype=torch.int64, device=dev)
+    slot_begin[1:] = torch.cumsum(cnt, 0)
+    if n == 0:
+        z32, z64 = torch.zeros(1, dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int64,
+                                                                              device=dev)
+        return slot_begin, (z32, z64, z64, 0)
+    crow = torch.repeat_interleave(torch.arange(len(ln), device=dev), cnt)
+    j = torch.arange(n, device=dev) - slot_begin[:-1][crow]
+    cb = begin[crow] + j * chunk
+    ce = torch.minimum(cb + chunk, end[crow])
+    return slot_begin, (row_ids[crow].to(torch.int32).contiguous(), cb.contiguous(),
+                        ce.contiguous(), n)
+
+
+def split_schedule(block: RatingBlock, seg: torch.Tensor, n_src_early: int,
+                   chunk: int = DEFAULT_CHUNK) -> SplitSchedule:
+    """The two-segment schedule of `block` (its rows' ratings ordered early-first, seg[r]
+    = end of row r's early segment)."""
+    dev = block.row_ptr.device
+    n = block.n_rows
+    rp = block.row_ptr
+    seg = seg.to(dev, torch.int64)
+    rows = torch.arange(max(n, 1), dtype=torch.int32, device=dev)
+    sb1, early = _segment_tasks(rows[:n], rp[:-1], seg, chunk, dev)
+    sb2, late = _segment_tasks(rows[:n], seg, rp[1:], chunk, dev)
+    sb2 = sb2 + early[3]
+    return SplitSchedule(int(n_src_early), rows, sb1.to(torch.int32).contiguous(),
+                         sb2.to(torch.int32).contiguous(), early, late)
+
+
+def solve_half_split(block: RatingBlock, sched: SplitSchedule, part: str, Y: torch.Tensor,
+                     X: torch.Tensor, rank: int, reg: float, implicit: bool, alpha: float,
+                     yty: Optional[torch.Tensor], status: torch.Tensor, ws: Workspace) -> None:
+    """One half of a two-segment half-sweep (ABI 6).  part "early": the early segments'
+    task partials from the first sched.n_src_early rows of Y (PREP over that prefix,
+    RSCALE, LAUNCH1), while the rest of Y may still be arriving; "late": the late
+    segments' partials from all of Y, then every row's slots summed and solved
+    (LAUNCH2) and the rescue (RESCUE, over the row's full ratings).  Both calls on
+    the same workspace, early first, in stream order."""
+    L = _lib.lib()
+    n = block.n_rows
+    w = ws.get(L.als_solve_workspace_bytes(rank, sched.n_slots, Y.shape[0], n))
+    if part == "early":
+        crow, cb, ce, nt = sched.early
+        ph, slot0, sb2, n_src = PHASE_PREP | PHASE_RSCALE | PHASE_LAUNCH1, 0, None, sched.n_src_early
+    elif part == "late":
+        crow, cb, ce, nt = sched.late
+        ph = PHASE_PREP | PHASE_RSCALE | PHASE_LAUNCH1 | PHASE_LAUNCH2 | PHASE_RESCUE
+        slot0, sb2, n_src = sched.early[3], sched.slot_begin2, Y.shape[0]
+    else:
+        raise ValueError(f"part must be 'early' or 'late', got {part!r}")
+    check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
+                           ptr(block.light_rows), 0, 0, ptr(sched.rows), ptr(sched.slot_begin), n,
+                           ptr(crow), ptr(cb), ptr(ce), nt, ptr(sb2), slot0,
+                           ptr(Y), n_src, ptr(X), X.shape[1], rank, float(reg),
+                           int(bool(implicit)), float(alpha), ptr(yty), ptr(status), ptr(w),
+                           w.numel(), int(ph), stream_ptr(X.device)), "als_solve_half (split)")
 
 
 def raise_status(s: int, where: str = "") -> None:

@@ -70,7 +70,8 @@ def test_workspace_sizes_are_monotone_and_host_only():
 def _solve_args(**over):
     a = dict(row_ptr=1, col=1, val=16, light=1, n_light=1, n_light_primal=1, heavy=1, slot=1,
              n_heavy=0, crow=1,
-             cbeg=1, cend=1, n_chunks=0, Y=16, n_src=0, X=16, ld=64, k=64, reg=0.1, implicit=0, alpha=1.0,
+             cbeg=1, cend=1, n_chunks=0, slot2=0, slot0=0, Y=16, n_src=0, X=16, ld=64, k=64,
+             reg=0.1, implicit=0, alpha=1.0,
              yty=0, status=1, ws=1, ws_bytes=1 << 20, phases=3, stream=0)
     a.update(over)
     return list(a.values())
@@ -85,7 +86,8 @@ def _solve_args(**over):
     (dict(n_light_primal=2), -1), (dict(n_light_primal=-1), -1),
     (dict(n_light_primal=0, k=32, ld=32), -1),           # dual path needs k > 32
     (dict(n_light_primal=0, k=128, ld=128, reg=0.0), -1),  # ... and regParam > 0
-    (dict(n_light_primal=0, k=128, ld=128, implicit=1, yty=8), -1)])  # ... and explicit
+    (dict(n_light_primal=0, k=128, ld=128, implicit=1, yty=8), -1),  # ... and explicit
+    (dict(slot0=-1), -1), (dict(slot0=1 << 20, ws_bytes=16), -2)])  # two-segment slots
 def test_solve_half_argument_errors(over, code):
     L = _lib.lib()
     rc = L.als_solve_half(*_solve_args(**over))

@@ -46,6 +46,35 @@ class OracleKernels:
         x = self.O.solve(A, b, ne, reg, None if yty is None else yty.numpy())
         X[:n, :rank] = torch.as_tensor(x)
 
+    def split_schedule(self, block, seg, n_src_early):
+        return {"seg": np.asarray(seg.cpu()), "n_src_early": int(n_src_early), "part": None}
+
+    def solve_split(self, block, sched, part, Y, X, rank, reg, implicit, alpha, yty, status,
+                    key):
+        """Two-segment half-sweep: the early part's normal equations from the early
+        rating segments with every source row past n_src_early poisoned (NaN: the early
+        part must never read the chunk still in flight), the late part's added in fp64."""
+        ptr, idx, val = block
+        n = len(ptr) - 1
+        if n == 0:
+            return
+        row_of = np.repeat(np.arange(n), np.diff(ptr))
+        early = np.arange(len(idx)) < sched["seg"][row_of]
+        mask = early if part == "early" else ~early
+        sub = np.zeros(n + 1, dtype=np.int64)
+        sub[1:] = np.cumsum(np.bincount(row_of[mask], minlength=n))
+        Ym = Y[:, :rank].numpy().copy()
+        if part == "early":
+            Ym[sched["n_src_early"]:] = np.nan
+        A, b, ne = self.O.normal_equations(sub, idx[mask], val[mask], Ym, implicit, alpha)
+        if part == "early":
+            sched["part"] = (A, b, ne)
+            return
+        A0, b0, ne0 = sched["part"]
+        sched["part"] = None
+        x = self.O.solve(A0 + A, b0 + b, ne0 + ne, reg, None if yty is None else yty.numpy())
+        X[:n, :rank] = torch.as_tensor(x)
+
     def predict(self, u_keys, i_keys, umap, imap, U, V, rank):
         u, i = u_keys.long(), i_keys.long()
         ok = (u >= 0) & (i >= 0)
@@ -81,7 +110,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, implicit, chunks, out_dir):
+def _worker(rank, world, port, implicit, chunks, out_dir, pipeline=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -97,7 +126,8 @@ def _worker(rank, world, port, implicit, chunks, out_dir):
         r = (r - 2.5).astype(np.float32)
     # arbitrary (non-aligned) input sharding: interleaved ratings
     sel = np.arange(len(u)) % world == rank
-    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=chunks)
+    K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=chunks,
+                   pipeline=pipeline)
     from oracle import als_oracle as O
     n_users = len(np.unique(u))
     U0 = O.initialize(n_users, 6, seed=2)
@@ -108,7 +138,7 @@ def _worker(rank, world, port, implicit, chunks, out_dir):
         np.savez(os.path.join(out_dir, f"dist_{int(implicit)}_{chunks}_{world}.npz"), uid=uid.numpy(),
                  U=Uf.numpy(), iid=iid.numpy(), V=Vf.numpy(), nnz=K.nnz,
                  u_starts=K.users.starts.numpy(), i_starts=K.items.starts.numpy(),
-                 local=[K.user_rows, K.item_rows])
+                 local=[K.user_rows, K.item_rows], pipeline=K.pipeline)
     dist.destroy_process_group()
 
 
@@ -184,15 +214,22 @@ def test_sharded_serving_matches_oracle(tmp_path, world):
     np.testing.assert_array_equal(d["sids"][0], uids[ref_u[0]])
 
 
-@pytest.mark.parametrize("implicit,chunks,world", [(False, None, 2), (True, None, 2), (False, 3, 2),
-                                                  (True, 3, 2), (False, 2, 8), (True, None, 8)])
-def test_sharded_als_matches_single_process(tmp_path, implicit, chunks, world):
-    """chunks=3: the [C, world, rows] layout with async per-chunk all-gathers.  world 8:
-    the target world size of BASELINE configs[3] (8 x MI355X), every rank a range of
+@pytest.mark.parametrize("implicit,chunks,world,pipeline",
+                         [(False, None, 2, None), (True, None, 2, None), (False, 3, 2, None),
+                          (True, 3, 2, None), (False, 3, 2, False), (True, 3, 2, False),
+                          (False, 2, 8, None), (True, 2, 8, None), (True, None, 8, None)])
+def test_sharded_als_matches_single_process(tmp_path, implicit, chunks, world, pipeline):
+    """chunks=3: the [C, world, rows] layout with async per-chunk all-gathers; with
+    several ranks and >= 2 chunks the item half-sweep is pipelined (default): the item
+    rows' early partials (users of chunks 0..C-2, every later source row poisoned with
+    NaN in the oracle kernels) are formed while the last user chunk's all-gather is in
+    flight, the late ones after; pipeline=False runs the plain chunked exchange.  world
+    8: the target world size of BASELINE configs[3] (8 x MI355X), every rank a range of
     ~15 users and ~11 items, the full 3-iteration fit against the single-process oracle."""
-    mp.spawn(_worker, args=(world, _free_port(), implicit, chunks, str(tmp_path)), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, _free_port(), implicit, chunks, str(tmp_path), pipeline),
+             nprocs=world, join=True)
     d = np.load(tmp_path / f"dist_{int(implicit)}_{chunks}_{world}.npz")
+    assert bool(d["pipeline"]) == (chunks is not None and pipeline is None)
     from oracle import als_oracle as O
     u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
     if implicit:

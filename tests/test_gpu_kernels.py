@@ -437,6 +437,62 @@ def test_rescue_list_emptied_between_row_chunks():
     assert counts[0] > 0 and counts[0] == counts[1], counts
 
 
+@pytest.mark.parametrize("implicit", [False, True])
+@pytest.mark.parametrize("rank", [8, 16, 48, 64, 100, 128])
+def test_two_segment_half_sweep(rank, implicit):
+    """ABI 6 two-segment schedule (the sharded engine's pipelined item side): every
+    item row's ratings ordered early-first — users below a cut (the arrived prefix of
+    Y), then the rest — the early call reads only that prefix (the rows past it hold NaN
+    during the call, as a chunk still in flight would hold anything), the late call
+    adds the remaining partials, sums every row's slots in fp64 and solves.  Against
+    the one-call solve of the same block and the fp64 oracle; chunk 64 so long rows
+    span several tasks of each segment, including the heavy item."""
+    u, i, r = planted(600, 200, density=0.08, heavy_items=(3,), seed=61)
+    if implicit:
+        r = (r - 2.5).astype(np.float32)
+    cut = 360  # users [0, cut) are the early prefix (dense user rows = ids here)
+    late = u >= cut
+    o = np.argsort(late, kind="stable")  # early ratings first in every row (stable CSR)
+    core = _core(u[o], i[o], r[o], chunk=64)
+    assert core.uidx.n == 600
+    core.init_factors(rank, seed=7)
+    ib = core.item_block
+    rp = ib.row_ptr.cpu().numpy()
+    col = ib.col.cpu().numpy()
+    seg = rp[:-1] + np.add.reduceat((col < cut).astype(np.int64), rp[:-1]) * (np.diff(rp) > 0)
+    assert (col[np.arange(len(col)) < np.repeat(seg, np.diff(rp))] < cut).all()
+    sched = E.split_schedule(ib, _t(seg, torch.int64), cut, chunk=64)
+    yty = E.compute_yty(core.U, core.n_users, rank, core.ws) if implicit else None
+    alpha = 2.0
+    # one-call reference on the same block
+    core.status.zero_()
+    E.solve_half(ib, core.U, core.V, rank, 0.1, implicit, alpha, yty, core.status, core.ws,
+                 dual=False)
+    V1 = core.V.clone()
+    U0 = core.U[:, :rank].cpu().numpy()
+    ws = E.Workspace(DEV)
+    Vs = torch.full_like(core.V, 7.0)
+    held = core.U[cut:].clone()
+    core.U[cut:] = float("nan")
+    E.solve_half_split(ib, sched, "early", core.U, Vs, rank, 0.1, implicit, alpha, yty,
+                       core.status, ws)
+    core.U[cut:] = held  # the last chunk "arrives" (stream order)
+    E.solve_half_split(ib, sched, "late", core.U, Vs, rank, 0.1, implicit, alpha, yty,
+                       core.status, ws)
+    torch.cuda.synchronize()
+    core.check_status()
+    Vs_np = Vs[:, :rank].cpu().numpy()
+    assert np.all(Vs[:, rank:].cpu().numpy() == 0.0)
+    V_ref = O.half_sweep(rp, col, ib.val.cpu().numpy(), U0, 0.1, implicit, alpha)
+    e_one = float(_exact_rel_errs(Vs_np, V1[:, :rank].cpu().numpy()).max())
+    e_ref = float(_exact_rel_errs(Vs_np, V_ref).max())
+    report(f"two_segment[rank={rank},imp={int(implicit)}]",
+           {"vs_one_call": e_one, "vs_oracle": e_ref, "early_tasks": sched.early[3],
+            "late_tasks": sched.late[3]})
+    assert sched.early[3] > 0 and sched.late[3] > 0
+    assert e_ref <= (1e-5 if implicit and rank <= 64 else 1e-4) and e_one <= 1e-4, (e_one, e_ref)
+
+
 @pytest.mark.parametrize("rank", [16, 64, 128])
 def test_rescue_list_overflow_is_an_error(rank):
     """A caller that runs the LAUNCH phases twice without RESCUE between them appends

@@ -315,7 +315,7 @@ class ShardedALS:
         # of chunk C-1 (late), so the early partial normal equations are formed while
         # the last user chunk's all-gather is still in flight (_pipelined_items)
         if pipeline is None:
-            pipeline = self.world > 1
+            pipeline = self._pipeline_pays(ri_, rc_)
         self.pipeline = bool(pipeline) and self.users.chunks >= 2
         self.item_split = None
         self.item_blocks = self._blocks(self.items, ri_, rc_, rv_, self.users,
@@ -327,6 +327,37 @@ class ShardedALS:
         self._dense_cache = {}
 
     # ---- setup helpers ----
+    # exchange model of the pipelining choice (unmeasured on a multi-GPU
+    # node): a ring all-gather over xGMI at RING_GBS per rank, partial slots at HBM_GBS
+    RING_GBS = 150.0
+    HBM_GBS = 5000.0
+
+    @classmethod
+    def pipeline_pays(cls, world: int, chunks: int, user_rows_per_chunk: int,
+                      item_rows: int, item_nnz: int, rank: int = 128) -> bool:
+        """Pipeline the item half-sweep when the exchange it hides — U chunk C-1's
+        all-gather, (W - 1) x a chunk's rows per rank — costs more than twice the
+        partial-slot traffic it adds (every item row through the slot path: about three
+        passes over one slot per <= 2048-rating segment, two segments per row)."""
+        if world < 2 or chunks < 2:
+            return False
+        ld = (rank + 3) // 4 * 4
+        recv = (world - 1) * user_rows_per_chunk * ld * 4
+        segs = 2 * max(item_rows, 1) + item_nnz // 2048
+        cn = 1 if rank <= 16 else (2 if rank <= 32 else (4 if rank <= 64 else 8))
+        slot = (cn * (cn + 1) // 2 * 4 + cn + 1) * 64 * 4
+        t_ring = recv / (cls.RING_GBS * 1e9)
+        t_slots = 3 * segs * slot / (cls.HBM_GBS * 1e9)
+        return t_slots < 0.5 * t_ring
+
+    def _pipeline_pays(self, rows_pad, cols_pad) -> bool:
+        """pipeline_pays for this rank's item rows at rank 128 (the factor rank is not
+        known yet), agreed by every rank (MIN)."""
+        ok = self.pipeline_pays(self.world, self.users.chunks, self.users.rows_per_chunk,
+                                self._local_rows(self.items), int(rows_pad.numel()))
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=self.device)
+        all_reduce_capped(flag, "pipeline choice", dist.ReduceOp.MIN, self.group)
+        return bool(int(flag))
     def _auto_chunks(self, u_space: int, i_space: int) -> int:
         """4 row chunks when a rank's share of the larger id space reaches 1M rows
         (the all-gather then moves >= 256 MB per rank at rank 64); 2 from 4 ranks on

@@ -3141,14 +3141,17 @@ static size_t slot_bytes(int32_t k, int32_t n_chunks) {
 }
 
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows) {
-  // 256 B of scale words (max |Y_src|, max |rating|, rescue count) | C-layout YtY
-  // (W1 implicit) | partial slots of the heavy-row chunks (n_chunks, counted from
-  // slot 0: chunk_slot0 + the call's chunks) | rescue list (n_rows) | split table
-  // ((n_src + 1) x k_pad words, explicit).  The slots sit at a fixed offset, so the
-  // two calls of a two-segment half-sweep (different n_src) share them.
+  // From the front: 256 B of scale words (max |Y_src|, max |rating|, rescue count) |
+  // C-layout YtY (W1 implicit) | partial slots of the heavy-row chunks (n_chunks,
+  // counted from slot 0: chunk_slot0 + the call's chunks) | rescue list (n_rows).
+  // From the back: the split table ((n_src + 1) x k_pad words, explicit), ending at
+  // the workspace's end (256-B aligned; + 256 B of slack for that alignment).  Calls
+  // that share one PREP (row chunks of a half-sweep: same Y_src, any n_chunks / n_rows)
+  // find the table at the same place, and the two calls of a two-segment half-sweep
+  // (different n_src) find the early partial slots at the same place.
   return 256 + ytyc_bytes(k) + slot_bytes(k, n_chunks) +
          align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0)) +
-         solve_table_bytes(k, n_src);
+         solve_table_bytes(k, n_src) + 256;
 }
 
 int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -3200,8 +3203,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
                                                     slot_bytes(k, n_slots));
   uint32_t* Ysp = reinterpret_cast<uint32_t*>(
-      reinterpret_cast<char*>(rescue_list) +
-      align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0)));
+      static_cast<char*>(ws) + ((ws_bytes - solve_table_bytes(k, n_src)) & ~(size_t)255));
   unsigned* rescue_cnt = scal_u + 2;
   const RescueList rl{rescue_cnt, rescue_list, (unsigned)(n_light + n_heavy)};
   // the rescue list (count at scale word 2, the rescue launch's finished-block counter

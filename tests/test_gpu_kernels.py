@@ -437,6 +437,44 @@ def test_rescue_list_emptied_between_row_chunks():
     assert counts[0] > 0 and counts[0] == counts[1], counts
 
 
+@pytest.mark.parametrize("rank", [16, 64, 128])
+def test_blocks_sharing_one_prep(rank):
+    """Row chunks of one half-sweep (the sharded engine's per-chunk blocks) share one Y
+    prep: the second call skips PREP and must find the split table where the first call
+    left it although the blocks differ in rows and heavy-row chunks (the table sits at
+    the workspace's end; round 5 briefly placed it after the per-call slot / rescue
+    regions, which moved it between such calls)."""
+    from als_mi355x.distributed import HipKernels
+    u, i, r = planted(700, 260, density=0.06, heavy_items=(3, 4, 5), seed=71)
+    K = HipKernels(DEV, chunk=64)
+    n_u = int(u.max()) + 1
+    V0 = torch.zeros((n_u, E.ld_for(rank)), device=DEV)
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    V0[:, :rank] = torch.randn((n_u, rank), generator=g, device=DEV)
+    parts = []
+    for lo, hi in ((0, 40), (40, 260)):  # 40 rows incl. the heavy items, then 220 rows
+        sel = (i >= lo) & (i < hi)
+        blk = K.build_block(_t(i[sel] - lo, torch.int32), _t(u[sel], torch.int32),
+                            _t(r[sel], torch.float32), hi - lo, n_u)
+        parts.append(blk)
+    assert parts[0].n_chunks > 0 and parts[0].n_light + parts[0].n_heavy != \
+        parts[1].n_light + parts[1].n_heavy
+    st = torch.zeros(1, dtype=torch.int32, device=DEV)
+    shared = [torch.full((b.n_rows, V0.shape[1]), 7.0, device=DEV) for b in parts]
+    for c, blk in enumerate(parts):
+        K.solve_half(blk, V0, shared[c], rank, 0.1, False, 1.0, None, st, first=(c == 0))
+    alone = []
+    for blk in parts:
+        X = torch.full((blk.n_rows, V0.shape[1]), 7.0, device=DEV)
+        E.solve_half(blk, V0, X, rank, 0.1, False, 1.0, None, st, E.Workspace(DEV))
+        alone.append(X)
+    torch.cuda.synchronize()
+    assert int(st.item()) == 0
+    for a, b in zip(shared, alone):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("implicit", [False, True])
 @pytest.mark.parametrize("rank", [8, 16, 48, 64, 100, 128])
 def test_two_segment_half_sweep(rank, implicit):

@@ -1322,16 +1322,24 @@ __device__ __forceinline__ float sweep16(float (&R)[16], Hook&& hook, float& dse
   return dmin;
 }
 
-// x of row group G broadcast to all four row groups (two VALU lane swaps:
-// v_permlane32_swap gives rows {0,1} (or {2,3}) in both halves, v_permlane16_swap then
-// row 2h (or 2h+1) in all four).
+// x of row group G broadcast to all four row groups: one ds_bpermute (the LDS
+// crossbar, not the VALU).  The sweep is bound by VALU issue, not by its pivot chain's
+// latency (three waves per SIMD hide it): two v_permlane*_swap plus their operand
+// copies (five VALU instructions per pivot) measured 0.06 ms slower on the configs[1]
+// user launch (A/B round 5, profiles/r05/ab_sweep_lean.jsonl).
 template <int G>
 __device__ __forceinline__ float rowgroup_bcast(float x) {
-  uint32_t a = __builtin_bit_cast(uint32_t, x), b = a;
-  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
-  uint32_t c = G < 2 ? a : b, d = c;
-  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(c), "+v"(d));
-  return __builtin_bit_cast(float, (G & 1) ? d : c);
+  const int src = (16 * G + (threadIdx.x & 15)) << 2;
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, x)));
+}
+
+// v on lanes with (lane & 15) == P, else -w.
+template <int P>
+__device__ __forceinline__ float sel_lane16_n(float v, float w) {
+  float r;
+  const uint64_t msk = 0x0001000100010001ull << P;
+  asm volatile("v_cndmask_b32_e64 %0, -%2, %1, %3" : "=v"(r) : "v"(v), "v"(w), "s"(msk));
+  return r;
 }
 
 // v on the lanes of 64-bit mask M (a constant), else w.
@@ -1349,7 +1357,13 @@ __device__ __forceinline__ float sel_mask(float v, float w) {
 // lane updates its four entries, not sixteen replicated ones, and the block never goes
 // through LDS (the result is already in the C layout the Pm / Schur MFMAs read).  Every
 // entry sees the same fp32 operations, in the same order, as in sweep16 (deferred
-// pivot-column scaling, look-ahead of the next pivot).
+// pivot-column scaling, look-ahead of the next pivot).  Per pivot the VALU issues the
+// four row updates, the pivot broadcast, its reciprocal, one multiply and the selects
+// (the multiplier's negation rides in a select's source modifier); positivity of the
+// pivots is checked by the caller from the spread test's minimum (dself_out), so the
+// returned minimum is not tracked here (+inf).  A 2 x 2-pivot form (8 sequential steps
+// instead of 16) measured slower: the same updates plus a 2 x 2 inverse per pair, and
+// the sweep is issue-bound, not chain-bound (A/B round 5, profiles/r05/ab_pair_pivots.jsonl).
 template <class Hook>
 __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
   // Bv was just written by the matrix cores (the pivot block's Schur update) and is
@@ -1363,11 +1377,10 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
   float d = bcast16<0>(rowp);
   float rd = rcp_t(d);
   float f = rowp * rd;
-  float nf = sel_lane16<0>(0.f, -f);
+  float nf = sel_lane16_n<0>(0.f, f);
   static_for<16>([&](auto pc) {
     constexpr int p = decltype(pc)::value;
     constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
-    dmin = fminf(dmin, d);
     asm volatile("s_nop 1" ::: "memory");
     // the register holding row p+1 first: then pivot p+1's row is final
     fmac_bcast16<p>(B[rn], nf);
@@ -1378,7 +1391,7 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
       dn = bcast16<p + 1>(rown);
       rdn = rcp_t(dn);
       fn = rown * rdn;
-      nfn = sel_lane16<p + 1>(0.f, -fn);
+      nfn = sel_lane16_n<p + 1>(0.f, fn);
     }
     static_for<4>([&](auto rc) {
       constexpr int r = decltype(rc)::value;
@@ -1396,7 +1409,6 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
   dself_out = dself;
   return dmin;
 }
-
 
 // Schur tiles of step K, I-major: u = 0 is (K+1, K+1), the next pivot block.
 template <int NB>
@@ -1799,7 +1811,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   rmax = fmaxf(rmax, dpp_f<0x141>(rmax));
   rmin = fminf(rmin, dpp_f<0x140>(rmin));
   rmax = fmaxf(rmax, dpp_f<0x140>(rmax));
-  return dmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;
+  return dmin > 0.f && rmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;
 }
 
 // w1_solve_x, then the solution row written un-permuted: dim d = i * NB + c <->

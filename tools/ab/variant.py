@@ -13,6 +13,28 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "..", "recommender-system-using-apache-spark-mllib-_amd", "csrc")
 GS = "gram_solve.hip"
 
+NEG = [
+        (GS, """// v on the lanes of 64-bit mask M (a constant), else w.""",
+         """// v on lanes with (lane & 15) == P, else -w.
+template <int P>
+__device__ __forceinline__ float sel_lane16_n(float v, float w) {
+  float r;
+  const uint64_t msk = 0x0001000100010001ull << P;
+  asm volatile("v_cndmask_b32_e64 %0, -%2, %1, %3" : "=v"(r) : "v"(v), "v"(w), "s"(msk));
+  return r;
+}
+
+// v on the lanes of 64-bit mask M (a constant), else w."""),
+        (GS, "  float nf = sel_lane16<0>(0.f, -f);\n  static_for<16>([&](auto pc) {\n    constexpr int p = decltype(pc)::value;\n    constexpr int qp",
+         "  float nf = sel_lane16_n<0>(0.f, f);\n  static_for<16>([&](auto pc) {\n    constexpr int p = decltype(pc)::value;\n    constexpr int qp"),
+        (GS, "      nfn = sel_lane16<p + 1>(0.f, -fn);\n    }\n    static_for<4>",
+         "      nfn = sel_lane16_n<p + 1>(0.f, fn);\n    }\n    static_for<4>"),
+        (GS, "    constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;\n    dmin = fminf(dmin, d);",
+         "    constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;"),
+        (GS, "  return dmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;",
+         "  return dmin > 0.f && rmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;"),
+    ]
+
 VARIANTS = {
     "base": [],
     # the round-4 rescue guards off: no split-window / rank-deficiency tests, no
@@ -25,7 +47,51 @@ VARIANTS = {
         (GS, "  return dmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;",
          "  return dmin > 0.f && __ballot(!fin) == 0;"),
     ],
+    # the C-layout sweep's row-group broadcast through the LDS crossbar (one
+    # ds_bpermute) instead of two VALU lane swaps and their copies
+    "bperm": [
+        (GS, """template <int G>
+__device__ __forceinline__ float rowgroup_bcast(float x) {
+  uint32_t a""", """template <int G>
+__device__ __forceinline__ float rowgroup_bcast(float x) {
+  if constexpr (true) {
+    const int src = (16 * G + (threadIdx.x & 15)) << 2;
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, x)));
+  }
+  uint32_t a"""),
+    ],
+    # the sweep's multiplier negation folded into its select, no per-pivot min (the
+    # pivots' positivity from the spread test's own minimum)
+    "neg": NEG,
+    "lean": None,  # bperm + neg
+    # timing bounds for the k <= 64 solve (wrong results): the C-layout sweep's pivot
+    # chain removed (the interleaved Schur MFMAs kept), or only its row-group broadcast
+    "fastsweep": [
+        (GS, "  if ((threadIdx.x & 63) == 0) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);",
+         "  if (false) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);"),
+        (GS, """    dmin = fminf(dmin, d);
+    asm volatile("s_nop 1" ::: "memory");
+    // the register holding row p+1 first: then pivot p+1's row is final
+    fmac_bcast16<p>(B[rn], nf);""", """    dmin = fminf(dmin, d);
+    if constexpr (true) { hook(pc); return; }
+    asm volatile("s_nop 1" ::: "memory");
+    // the register holding row p+1 first: then pivot p+1's row is final
+    fmac_bcast16<p>(B[rn], nf);"""),
+    ],
+    "noperm": [
+        (GS, "  if ((threadIdx.x & 63) == 0) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);",
+         "  if (false) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);"),
+        (GS, """template <int G>
+__device__ __forceinline__ float rowgroup_bcast(float x) {
+  uint32_t a""", """template <int G>
+__device__ __forceinline__ float rowgroup_bcast(float x) {
+  if constexpr (true) return x;
+  uint32_t a"""),
+    ],
 }
+
+
+VARIANTS["lean"] = VARIANTS["bperm"] + VARIANTS["neg"]
 
 
 def build(tag: str) -> str:
@@ -53,10 +119,19 @@ def build(tag: str) -> str:
     lib = os.path.join(HERE, f"libals_{tag}.so")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-shared", "-fPIC", "--offload-arch=gfx950"] + objs
                           + ["-o", lib])
+    if "--dev" in sys.argv:  # the phase-ablation kernels (tools/dev_ablate.hip) on this copy
+        dev_src = os.path.join(src, "dev_ablate.hip")
+        s = open(os.path.join(HERE, "..", "dev_ablate.hip")).read().replace(
+            '"../recommender-system-using-apache-spark-mllib-_amd/csrc/gram_solve.hip"',
+            '"gram_solve.hip"')
+        open(dev_src, "w").write(s)
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-fPIC", "-shared",
+                               "--offload-arch=gfx950", "-std=c++17", dev_src, "-o",
+                               os.path.join(HERE, f"libals_dev_{tag}.so")])
     shutil.rmtree(src)
     return lib
 
 
 if __name__ == "__main__":
-    for t in sys.argv[1:]:
+    for t in [a for a in sys.argv[1:] if not a.startswith("--")]:
         print("built", build(t), flush=True)

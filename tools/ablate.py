@@ -18,6 +18,8 @@ _pkgload.load()
 from als_mi355x import datasets as D, engine as E  # noqa: E402
 
 SO = os.path.join(ROOT, "tools", "libals_dev.so")
+if "--lib" in sys.argv:  # a tools/ab/variant.py --dev build
+    SO = sys.argv[sys.argv.index("--lib") + 1]
 
 
 def build():
@@ -80,7 +82,7 @@ def main():
                 assert rc == 0, rc
                 times.append(e0.elapsed_time(e1))
             t = sorted(times[1:])[1]
-            print(f"rank {k} {side:5s} rows={n:7d} mode {mode} {names[mode]:11s} {t:8.3f} ms"
+            print(f"{os.path.basename(SO)} rank {k} {side:5s} rows={n:7d} mode {mode} {names[mode]:11s} {t:8.3f} ms"
                   f"  {1e6 * t / max(n, 1):8.2f} ns/row", flush=True)
 
 

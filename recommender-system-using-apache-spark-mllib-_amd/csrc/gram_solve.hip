@@ -1449,16 +1449,15 @@ __host__ __device__ constexpr int schur_J(int K, int u) {
 template <int NB>
 constexpr bool kW1SplitSchur = NB == 8;
 // Diagonal blocks swept in the MFMA C layout (sweep16c: 4 entries per lane instead of
-// 16 replicated) for NB = 4: the k <= 64 solves and the 33-64-rating dual systems
-// (A/B round 4, `profiles/r04/ab_sweepc_classes.jsonl`: configs[1] 2.246 -> 2.203
-// ms/iter, configs[3] 294.6 -> 292.8 ms; with NB = 2 and 6 as well configs[3] went to
-// 299).  Not in the NB = 8 (W1) kernels: there the compiler keeps tiles in AGPRs and
-// copies them out right before the inline DPP asm, a hazard it does not see (2.2e-2
-// row errors measured; tests/test_isa_hazards.py scans for it), and with a nop in
-// front of every DPP statement they measured slower (configs[2] 9.03 -> 11.56 ms,
-// configs[3] 293 -> 300 ms, `profiles/r04/ab_sweepc_w1.jsonl`).
-template <int NB>
-constexpr bool kSweepC = NB == 4;
+// 16 replicated) in every elimination but the split-Schur one.  With the row-group
+// pivot broadcast as one ds_bpermute (round 5) it pays in the NB = 8 fp32 kernels too,
+// which round 4 (two permlane swaps per pivot) had measured slower: A/B round 5,
+// `profiles/r05/ab_sweepc_nb.jsonl`, configs[3] 287.4 -> 280.1 ms/iter (explicit
+// rank-128 user launch 101.5 -> 96.3 ms, dual systems 65.6 -> 64.7 ms), configs[1]
+// 2.043 -> 2.032.  In the split-Schur form (implicit rank-128 light rows, heavy-row
+// solves) it is slower: configs[2] 9.32 -> 10.99 ms/iter (user launch 5.48 -> 6.66).
+template <int NB, bool SPLIT>
+constexpr bool kSweepC = !SPLIT;
 // Measured round 4 (A/B at configs[1] / configs[3]): the split form in the explicit
 // k <= 64 solve (2.33 vs 2.26 ms/iter), the explicit rank-128 light rows (user launch
 // 112 vs 102 ms) and the n x n dual systems (76 vs 70 ms) is slower: fp32 stays there.
@@ -1654,7 +1653,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   floatx4 Gm, bk;
   auto pivot_block = [&](auto Kc, auto&& hook) {
     constexpr int K = decltype(Kc)::value;
-    if constexpr (kSweepC<NB>) {
+    if constexpr (kSweepC<NB, SPLIT>) {
       // swept in the C layout: Gm comes out where the MFMAs read it
       Gm = A[w1_tile<NB>(K, K)];
       float ds;

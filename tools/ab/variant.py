@@ -64,6 +64,14 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
     # pivots' positivity from the spread test's own minimum)
     "neg": NEG,
     "lean": None,  # bperm + neg
+    # C-layout sweeps (ds_bpermute broadcast) in every block elimination: NB = 2, 6, 8 too
+    # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
+    "sweepc_nb4": [
+        (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = NB == 4;"),
+    ],
+    "sweepc_all": [
+        (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = true;"),
+    ],
     # timing bounds for the k <= 64 solve (wrong results): the C-layout sweep's pivot
     # chain removed (the interleaved Schur MFMAs kept), or only its row-group broadcast
     "fastsweep": [

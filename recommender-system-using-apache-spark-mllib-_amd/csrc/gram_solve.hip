@@ -2125,7 +2125,8 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
 
 // (k <= 64 keeps one gather step in flight: two steps need 187 registers, i.e. two
 // waves per SIMD instead of three, measured slower on configs[1]: 2.07 -> 2.24 ms/iter.)
-// (Four waves per SIMD for explicit k <= 64 spill 49 registers: 2.76 vs 2.25 ms/iter.)
+// (Four waves per SIMD for explicit k <= 64 spill 49 registers: 2.76 vs 2.25 ms/iter;
+// round 5, after the lean sweep, 11 spills: 2.14 vs 2.02 ms/iter, profiles/r05/ab_occupancy.jsonl.)
 template <int CN, bool IMPLICIT>
 __global__ __launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,
@@ -2717,7 +2718,8 @@ __device__ __forceinline__ void dual_row(int row, int n, const int (&cj)[2],
 
 // One wavefront per short light row (the tail of the longest-first light list: every
 // row with <= kDualMaxRatings ratings at k in (64, 128], KP = 128; <= kDualMaxRatings64
-// at k in (32, 64], KP = 64), explicit, regParam > 0.
+// at k in (32, 64], KP = 64), explicit, regParam > 0.  (Three waves per SIMD: 27
+// spilled registers, configs[3] dual launch 64.8 -> 67.8 ms, profiles/r05/ab_occupancy.jsonl.)
 template <int KP>
 __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
     const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col,

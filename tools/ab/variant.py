@@ -65,6 +65,15 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
     "neg": NEG,
     "lean": None,  # bperm + neg
     # C-layout sweeps (ds_bpermute broadcast) in every block elimination: NB = 2, 6, 8 too
+    # occupancy: four waves per SIMD for the explicit k <= 64 kernel, three for the dual
+    "occ4": [
+        (GS, "__launch_bounds__(64, IMPLICIT ? 2 : 3) void gram_solve_kernel(",
+         "__launch_bounds__(64, IMPLICIT ? 2 : 4) void gram_solve_kernel("),
+    ],
+    "dual3": [
+        (GS, "__launch_bounds__(64, 2) void gram_solve_dual_kernel(",
+         "__launch_bounds__(64, 3) void gram_solve_dual_kernel("),
+    ],
     # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
     "sweepc_nb4": [
         (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = NB == 4;"),

@@ -17,9 +17,9 @@
 // so a staged tile row is copied as is and every B operand is one
 // ds_read_b128.  The query rows are split in registers once per workgroup.
 //
-// Workgroup = 4 wavefronts x RG row groups = 64 RG query rows.  The workgroup
-// sweeps V in tiles double-buffered in LDS (one barrier per tile, the loads of
-// the tile after next in flight).  V is swept in order of decreasing row norm
+// Workgroup = NW wavefronts x RG row groups = 16 NW RG query rows.  The workgroup
+// sweeps V in tiles double-buffered in LDS (one barrier per tile, the next tile's
+// LDS-DMA pieces in flight).  V is swept in order of decreasing row norm
 // (bucketed; the high-scoring rows come first, so the lists fill with
 // near-final entries early), each 16 x 16 score block is filtered against its
 // rows' current k-th best score, and the rare survivors are inserted into the
@@ -395,12 +395,12 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 //  * with register lists a workgroup is 8 wavefronts (128 RG query rows per tile
 //    stream; one workgroup per CU at the lists' register count) and a tile is 16-32
 //    KB, so each L2 latency delivers more rows.
-// Tiles are double-buffered in LDS: tile t+1 is written (from registers loaded one
-// tile earlier) while nothing reads its buffer, so ONE barrier per tile; the global
-// loads of tile t+2 are in flight during tile t+1's MFMAs.  LDS rows are RW + 2
-// uint4 apart (RW = 4 NK): the ds_read_b128 lane groups of gfx950
-// ({0-3,12-15,20-27}, ...) then touch 16 distinct 4-bank slots (row stride = 2 x odd
-// mod 16 slots), conflict-free.
+// Tiles are double-buffered in LDS and land there by LDS-DMA (global_load_lds_dwordx4,
+// no staging registers, no ds_write): tile t+1's pieces are issued right after the
+// barrier that released its buffer and fly while tile t is scored; ONE barrier per
+// tile.  Rows are unpadded (RW = 4 NK uint4) and swizzled (TK_SWZ), so the
+// ds_read_b128 lane groups of gfx950 ({0-3,12-15,20-27}, ...) touch 16 distinct 4-bank
+// slots, conflict-free.
 // Coarse filter, exact refinement: a block is first scored with hi.hi alone (one
 // MFMA per k-step instead of three).  The dropped terms hi.lo + lo.hi are bounded
 // by 2^-10 |q| |v| (Cauchy-Schwarz on |lo| <= 2^-11 |t|, plus the f16 subnormal
@@ -438,9 +438,24 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // wavefronts) 128 rows at NK = 4 (4 staged uint4 per thread), 256 / NK below (2 per
 // thread); LDS lists (4 wavefronts) 64 / NK rows (1 per thread), which leaves the
 // LDS to the lists.
+// (Round 5, LDS-DMA staging, configs[4] 262,144-user sample: 192-row tiles at rank >
+// 64 vs 128: top-10 91.5 -> 89.4 ms, top-100 193.5 -> 189.5 ms; 256 rows do not fit
+// the LDS beside the lo scratch and the score blocks.)
 __host__ __device__ constexpr int tk_vt(int nk, int topr) {
-  return topr == 0 ? 64 / nk : (nk == 4 ? 128 : 256 / nk);
+  return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 256 / nk);
 }
+// Tile buffers in LDS: the one scored and the next one landing.  (Three, i.e. two
+// tiles in flight, measured slower: top-100 203 vs 193 ms at 128-row tiles — a refined
+// block's vmcnt(0) then also waits for the later tile's pieces.)
+__host__ __device__ constexpr int tk_nbuf(int topr) { return topr == 0 ? 2 : 2; }
+
+// Tile-row swizzle: uint4 column c of tile row r sits at c ^ sw(r), sw(r) = (r >> 1) & 3
+// at RW = 4 (NK = 1), r & (RW - 1) at RW = 8, 16: the ds_read_b128 lane groups of gfx950
+// ({0-3,12-15,20-27}, ...) reading column 4s + q of rows 16b + m then touch 16 distinct
+// 16-byte bank slots (checked by enumeration for each RW).  (Written out where it is
+// used: a call to a function template from the kernel's lambdas made hipcc's host pass
+// drop the kernels' handles, an undefined symbol at load time.)
+#define TK_SWZ(NK, r) ((NK) == 1 ? ((r) >> 1) & 3 : (r) & (4 * (NK) - 1))
 
 // Insert key `c` into a list sorted ascending (the k-th best at [0]; sentinels past
 // `top`).  c_j = c > key_j is monotone (true for j < p); the list becomes
@@ -506,19 +521,21 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
                                                          int32_t* __restrict__ idx_out,
                                                          float* __restrict__ score_out) {
   constexpr int NW = tk_nw(TOPR);  // wavefronts
-  constexpr int NT = 64 * NW;          // threads
   constexpr int GR = 16 * NW;          // query rows of a row group
   constexpr int KQ = 32 * NK;
   constexpr int RW = KQ / 8;           // uint4 per row of a split plane (KQ halves)
-  constexpr int RS = RW + 2;           // LDS row stride in uint4 (bank-conflict-free)
   constexpr int VT = tk_vt(NK, TOPR);  // V rows per tile
   constexpr int NC = VT / 16;          // 16-row score blocks per tile
-  constexpr int PER = VT * RW / NT;    // staged uint4 per thread per tile
-  static_assert(PER * NT == VT * RW && VT <= NT, "tile staging");
+  constexpr int NI = VT * RW / 64;     // LDS-DMA wave-instructions (1 KB) per tile
+  constexpr int VP = VT < 64 ? 64 : VT;  // sweep-order indices staged per tile
+  static_assert(NI % NW == 0 && VP % 64 == 0, "tile staging");
   extern __shared__ uint4 smem_u4[];
-  uint4* tiles = smem_u4;                                     // [2][VT][RS]
-  int* tperm = reinterpret_cast<int*>(tiles + 2 * VT * RS);   // [2][VT] V row of each tile row
-  int* sdone = tperm + 2 * VT;                                // [2][NW] wave done flags
+  constexpr int NBUF = tk_nbuf(TOPR);  // tile buffers: tiles t + 1 .. t + NBUF - 1 in flight
+  // LDS-DMA loads per wave and tile: NI / NW pieces of V rows + one of sweep indices
+  constexpr int PIECES = NI / NW + 1;
+  uint4* tiles = smem_u4;                                       // [NBUF][VT][RW], swizzled
+  int* tperm = reinterpret_cast<int*>(tiles + NBUF * VT * RW);  // [NBUF][VP] V row of each tile row
+  int* sdone = tperm + NBUF * VP;                               // [2][NW] wave done flags
   float* sqs = reinterpret_cast<float*>(sdone + 2 * NW);      // [NW][RG][16] slack coefficients
   uint4* loscr = reinterpret_cast<uint4*>(sqs + GR * RG);     // [NW][NK][64] lo of a refined block
   // TOPR == 0: [GR RG rows][top] keys (best first), [GR RG] lengths
@@ -529,6 +546,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   float* sblk = reinterpret_cast<float*>(lk);
 
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int swz = TK_SWZ(NK, m);  // the swizzle of every tile row this lane reads (row % 16 = m)
   const int64_t qbase = (int64_t)blockIdx.x * GR * RG;
   const int eu = tk_split_exponent(scal[0]), ev = tk_split_exponent(scal[1]);
   const float su = ldexpf(1.f, eu), unscale = ldexpf(1.f, -eu - ev);
@@ -600,52 +618,52 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
 #pragma unroll
     for (int j = 0; j < NR; ++j) kv[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
 
-  // Tiles in flight in registers: DEPTH sets; after tile t is scored, tile t + 1 is
-  // staged from set t % DEPTH, which then loads tile t + 1 + DEPTH.  Two sets with
-  // register lists (the sweep is bound by the V bytes in flight), one with LDS lists.
-  constexpr int DEPTH = TOPR > 0 ? 2 : 1;
-  uint4 pre[DEPTH][PER];
-  int pre_p[DEPTH];
-  // norm of the first row of the fetched / current tile: V is sorted by decreasing
-  // norm, so x 2^(1/128) (one bucket) it bounds every row from that tile on
-  float nv_pre[DEPTH], nv_cur = 0.f;
-  auto fetch = [&](int64_t vb, auto dc) {
-    constexpr int D = decltype(dc)::value;
+  // Tile staging by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write): the
+  // workgroup's waves each issue NI / NW of the tile's 1 KB pieces.  Tile row r, uint4 c
+  // lands at r RW + (c ^ TK_SWZ(NK, r)) (one DMA piece = 64 consecutive uint4), so the
+  // B-operand reads stay conflict-free without padding.  Rows past n_v load row
+  // n_v - 1; their scores are masked to NaN (score), so no filter passes them.
+  auto issue_tile = [&](int64_t vb, int b) {
+    if (n_v <= 0) return;  // (every wave alike: the vmcnt counts below stay uniform)
+    uint4* t = tiles + b * VT * RW;
 #pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int x = threadIdx.x + NT * e;
-      const int64_t vrow = vb + x / RW;
-      // rows past n_v: f16 NaNs, so their scores are NaN and never pass a filter
-      pre[D][e] = vrow < n_v ? Vsp[vrow * RW + x % RW]
-                             : make_uint4(0x7E007E00u, 0x7E007E00u, 0x7E007E00u, 0x7E007E00u);
+    for (int e = 0; e < NI / NW; ++e) {
+      const int j = w * (NI / NW) + e;
+      const int x = 64 * j + lane;
+      const int r = x / RW;
+      const int64_t vr = vb + r < n_v ? vb + r : n_v - 1;
+      __builtin_amdgcn_global_load_lds(Vsp + vr * RW + ((x % RW) ^ TK_SWZ(NK, r)), t + 64 * j, 16,
+                                       0, 0);
     }
-    if (threadIdx.x < VT)
-      pre_p[D] = vb + threadIdx.x < n_v ? perm[vb + threadIdx.x] : 0x7fffffff;
-    nv_pre[D] = vnorm[vb];
-  };
-  auto stage = [&](int buf, auto dc) {
-    constexpr int D = decltype(dc)::value;
-    uint4* t = tiles + buf * VT * RS;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) {
-      const int x = threadIdx.x + NT * e;
-      t[(x / RW) * RS + x % RW] = pre[D][e];
+    {  // piece w % (VP / 64): waves sharing a piece write the same words
+      const int e = w % (VP / 64);
+      const int64_t vr = vb + 64 * e + lane;
+      __builtin_amdgcn_global_load_lds(perm + (vr < n_v ? vr : n_v - 1), tperm + b * VP + 64 * e,
+                                       4, 0, 0);
     }
-    if (threadIdx.x < VT) tperm[buf * VT + threadIdx.x] = pre_p[D];
-    nv_cur = nv_pre[D];
   };
+  // norm of the current tile's first row: V is sorted by decreasing norm, so x
+  // 2^(1/128) (one bucket) it bounds every row from that tile on
+  float nv_cur = 0.f;
   // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m (reading
   // the B operands one block ahead in registers measured no faster: the sweep is not
   // bound by LDS latency, and the quad kernel then spills)
-  auto score = [&](const uint4* tb, floatx4 (&acc)[RG]) {  // hi.hi
+  auto score = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG]) {  // hi.hi
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
-      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[(4 * s + q) ^ swz]);
 #pragma unroll
       for (int g = 0; g < RG; ++g)
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
+    }
+    if (ibase + 16 > n_v) {  // the last tile: rows past n_v score NaN
+      const bool past = ibase + m >= n_v;
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[g][r] = past ? __builtin_nanf("") : acc[g][r];
     }
   };
 
@@ -661,7 +679,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int s = 0; s < NK; ++s) {
-      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[4 * s + q]);
+      const tk_half8 bh = __builtin_bit_cast(tk_half8, tb[(4 * s + q) ^ swz]);
       const tk_half8 bl = __builtin_bit_cast(tk_half8, scr[s * 64 + lane]);
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
@@ -819,18 +837,20 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
     }
   };
 
-  using D0 = std::integral_constant<int, 0>;
-  using D1 = std::integral_constant<int, DEPTH - 1>;
-  fetch(0, D0{});
-  stage(0, D0{});
-  __syncthreads();
-  if (VT < n_v) fetch(VT, D0{});
-  if (DEPTH > 1 && 2 * VT < n_v) fetch(2 * VT, D1{});
-  int buf = 0;
-  // one tile: score + filter tile vb in buffer buf, stage tile vb + VT from register
-  // set D, barrier, load tile vb + (DEPTH + 1) VT into set D; false: sweep over
-  auto tile_step = [&](int64_t vb, auto dc) -> bool {
-      const uint4* tb = tiles + buf * VT * RS;
+  // tile t in buffer t % NBUF; tiles t + 1 .. t + NBUF - 1 are in flight while tile t is
+  // scored (tiles past the sweep too, clamped: every wave issues the same loads, so the
+  // vmcnt counts are exact); each wave waits for its own pieces of tile t + 1 before the
+  // barrier that ends tile t, which also releases tile t's buffer for tile t + NBUF
+  // (__syncthreads() would wait for every load in flight, the later tiles' included:
+  // the barriers here wait for this wave's LDS accesses and its pieces of one tile only)
+  for (int i = 0; i < NBUF; ++i) issue_tile(i * VT, i);
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(PIECES * (NBUF - 1)) : "memory");
+  int buf = 0, par = 0;
+  // one tile: score + filter tile vb in buffer buf, barrier, issue tile vb + NBUF VT into
+  // buffer buf; false: sweep over
+  auto tile_step = [&](int64_t vb) -> bool {
+      const uint4* tb = tiles + buf * VT * RW;
+      nv_cur = n_v > 0 ? vnorm[vb] : 0.f;
       nvt = fmaf(nv_cur, 1.01f, 1.f);
       // early exit: every row of the wave holds a k-th score that no row from this
       // tile on can reach: k-th > (|q| + 1)(NV + 1)(1 + 2^-7) (dead rows: +inf)
@@ -867,10 +887,10 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
           floatx4 a4[4][RG];
 #pragma unroll 1
           for (int c = 0; c < NC; c += 4) {
-            const uint4* tbr = tb + (16 * c + m) * RS;
-            const int* bp = tperm + buf * VT + 16 * c;
+            const uint4* tbr = tb + (16 * c + m) * RW;
+            const int* bp = tperm + buf * VP + 16 * c;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) score(tbr + 16 * j * RS, a4[j]);
+            for (int j = 0; j < 4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
             if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {
               bool any = false;
 #pragma unroll
@@ -883,44 +903,41 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
             }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              filter(a4[j], vb + 16 * (c + j), bp + 16 * j, tbr + 16 * j * RS);
+              filter(a4[j], vb + 16 * (c + j), bp + 16 * j, tbr + 16 * j * RW);
           }
         } else {
-        score(tb + m * RS, acc0);
+        score(tb + m * RW, vb, acc0);
         // block pairs: issue block c+1's MFMAs, then filter block c
 #pragma unroll 1
         for (int c = 0; c < NC; c += 2) {
-          const uint4* tbr = tb + (16 * c + m) * RS;
-          const int* bp = tperm + buf * VT + 16 * c;
-          if (NC > 1) score(tbr + 16 * RS, acc1);
+          const uint4* tbr = tb + (16 * c + m) * RW;
+          const int* bp = tperm + buf * VP + 16 * c;
+          if (NC > 1) score(tbr + 16 * RW, vb + 16 * c + 16, acc1);
           filter(acc0, vb + 16 * c, bp, tbr);
           if (NC > 1) {
-            if (c + 2 < NC) score(tbr + 32 * RS, acc0);
-            filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RS);
+            if (c + 2 < NC) score(tbr + 32 * RW, vb + 16 * c + 32, acc0);
+            filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RW);
           }
         }
         }
       }
-      if (vb + VT < n_v) stage(buf ^ 1, dc);
-      if (lane == 0) sdone[buf * NW + w] = wdone ? 1 : 0;
-      __syncthreads();
-      // (flags of this buffer are rewritten only after the next barrier)
+      // this wave's pieces of tile vb + VT (the later tiles' may stay in flight)
+      if (lane == 0) sdone[par * NW + w] = wdone ? 1 : 0;
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(PIECES * (NBUF - 2)) : "memory");
+      // (flags of this parity are rewritten only after the next barrier)
       int alldone = 1;
 #pragma unroll
-      for (int i = 0; i < NW; ++i) alldone &= sdone[buf * NW + i];
+      for (int i = 0; i < NW; ++i) alldone &= sdone[par * NW + i];
       if (alldone) return false;
-      if (vb + (DEPTH + 1) * VT < n_v) fetch(vb + (DEPTH + 1) * VT, dc);
-      buf ^= 1;
+      issue_tile(vb + NBUF * VT, buf);
+      buf = buf + 1 == NBUF ? 0 : buf + 1;
+      par ^= 1;
       return vb + VT < n_v;
   };
-  for (int64_t vb = 0;;) {
-    if (!tile_step(vb, D0{})) break;
-    vb += VT;
-    if constexpr (DEPTH > 1) {
-      if (!tile_step(vb, D1{})) break;
-      vb += VT;
-    }
-  }
+  for (int64_t vb = 0;; vb += VT)
+    if (!tile_step(vb)) break;
+  // no LDS-DMA may still be landing when the workgroup ends
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (QUAD) {
     // output position of a real entry = number of real entries above it in the
     // row's four sub-lists; open slots (fewer than `top` V rows) fill the tail
@@ -1036,9 +1053,10 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
   const int nw = topk_nw(top, quad, rg);
   const bool reg_lists = top <= kTopR || quad;
   const size_t vt = (size_t)tk_vt(nk, reg_lists ? 1 : 0);
-  // [2][vt] tile rows of KQ hi halves (stride kq/8 + 2 uint4) | [2][vt] V rows |
-  // [2][4] done flags | [4][rg][16] slack coefficients | [4][nk][64] uint4 lo scratch
-  const size_t tiles = 16 * 2 * vt * (size_t)(kq / 8 + 2) + 4 * 2 * vt + 4 * 2 * nw +
+  // [nbuf][vt] tile rows of KQ hi halves (kq/8 uint4) | [nbuf][max(vt, 64)] V rows |
+  // [2][nw] done flags | [nw][rg][16] slack coefficients | [nw][nk][64] uint4 lo scratch
+  const size_t nbuf = (size_t)tk_nbuf(reg_lists ? 1 : 0);
+  const size_t tiles = 16 * nbuf * vt * (size_t)(kq / 8) + 4 * nbuf * std::max<size_t>(vt, 64) + 4 * 2 * nw +
                        4 * 16 * nw * (size_t)rg + 16 * nw * 64 * (size_t)nk;
   if (reg_lists) return tiles + sizeof(float) * nw * (size_t)rg * (256 + 16);
   return tiles + sizeof(uint64_t) * 64 * (size_t)rg * top +

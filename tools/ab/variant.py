@@ -12,6 +12,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "..", "..", "recommender-system-using-apache-spark-mllib-_amd", "csrc")
 GS = "gram_solve.hip"
+TK = "topk.hip"
 
 NEG = [
         (GS, """// v on the lanes of 64-bit mask M (a constant), else w.""",
@@ -73,6 +74,101 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
     "dual3": [
         (GS, "__launch_bounds__(64, 2) void gram_solve_dual_kernel(",
          "__launch_bounds__(64, 3) void gram_solve_dual_kernel("),
+    ],
+    # top-k timing bound (wrong scores by the hi.lo term): refinement without the lo
+    # fetch (bl = 0), i.e. the cost of the lo loads' latency
+    "tk_nolo": [
+        (TK, """      __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");""", """      (void)vr;"""),
+        (TK, "const tk_half8 bl = __builtin_bit_cast(tk_half8, scr[s * 64 + lane]);",
+         "const tk_half8 bl = {};"),
+    ],
+    # top-k timing bound (no lists: wrong results): the sweep alone, every quartet
+    # scored (V stream, LDS, MFMA, barriers) and no block filtered
+    "tk_scoreonly": [
+        (TK, """            for (int j = 0; j < 4; ++j) score(tbr + 16 * j * RS, a4[j]);
+            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {""",
+         """            for (int j = 0; j < 4; ++j) score(tbr + 16 * j * RS, a4[j]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              asm volatile("" :: "v"(a4[j][0][0]), "v"(a4[j][0][1]), "v"(a4[j][0][2]), "v"(a4[j][0][3]));
+            if (true) continue;
+            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {"""),
+    ],
+    # top-k event counters (dev): quartets scored / past the coarse ballot, blocks
+    # refined, insertion passes, keys inserted (als_dev_tk_counters)
+    "tk_count": [
+        (TK, "namespace als {\n", "namespace als {\n__device__ unsigned long long tk_dbg[8];\n"),
+        (TK, "              if (__ballot(any) == 0) continue;",
+         """              if (lane == 0) atomicAdd(&tk_dbg[0], 1ull);
+              if (__ballot(any) != 0 && lane == 0) atomicAdd(&tk_dbg[1], 1ull);
+              if (__ballot(any) == 0) continue;"""),
+        (TK, """        if (__ballot(c) == 0) return;
+      }
+      refine(tbr, ibase, acc);""", """        if (__ballot(c) == 0) return;
+      }
+      if (lane == 0) atomicAdd(&tk_dbg[2], 1ull);
+      refine(tbr, ibase, acc);"""),
+        (TK, "          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv[g], c);",
+         """          const bool do_ins = c > gmin && q == (__builtin_ctzll(holders) >> 4);
+          {
+            const uint64_t bi = __ballot(do_ins);
+            if (lane == 0) {
+              atomicAdd(&tk_dbg[3], 1ull);
+              atomicAdd(&tk_dbg[4], (unsigned long long)__popcll(bi));
+            }
+          }
+          if (do_ins) tk_insert<NR>(kv[g], c);"""),
+        (TK, "}  // extern \"C\"\n", """int als_dev_tk_counters(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(als::tk_dbg), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(als::tk_dbg), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+}  // extern "C"
+"""),
+    ],
+    # top-k: 192-row tiles at rank > 64 (register / quad lists)
+    "tk_vt192": [
+        (TK, "return topr == 0 ? 64 / nk : (nk == 4 ? 128 : 256 / nk);",
+         "return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 256 / nk);"),
+        (TK, "constexpr int tk_nbuf(int topr) { return topr == 0 ? 2 : 3; }",
+         "constexpr int tk_nbuf(int topr) { return topr == 0 ? 2 : 2; }"),
+    ],
+    # top-k: both f16 planes of V staged in LDS (two buffers), refinement from LDS
+    # (no lo fetch, no wait on the tile loads in flight); twice the V stream
+    "tk_lolds": [
+        (TK, "constexpr int tk_nbuf(int topr) { return topr == 0 ? 2 : 3; }",
+         "constexpr int tk_nbuf(int topr) { return topr == 0 ? 2 : 2; }"),
+        (TK, "  constexpr int PIECES = NI / NW + 1;", "  constexpr int PIECES = 2 * (NI / NW) + 1;"),
+        (TK, "  int* tperm = reinterpret_cast<int*>(tiles + NBUF * VT * RW);",
+         "  int* tperm = reinterpret_cast<int*>(tiles + 2 * NBUF * VT * RW);"),
+        (TK, """      __builtin_amdgcn_global_load_lds(Vsp + vr * RW + ((x % RW) ^ TK_SWZ(NK, r)), t + 64 * j, 16,
+                                       0, 0);""", """      __builtin_amdgcn_global_load_lds(Vsp + vr * RW + ((x % RW) ^ TK_SWZ(NK, r)), t + 64 * j, 16,
+                                       0, 0);
+      __builtin_amdgcn_global_load_lds(Vlo + vr * RW + ((x % RW) ^ TK_SWZ(NK, r)),
+                                       t + NBUF * VT * RW + 64 * j, 16, 0, 0);"""),
+        (TK, """    const int64_t vr = ibase + m < n_v ? ibase + m : n_v - 1;  // rows past n_v: NaN anyway
+    uint4* scr = loscr + w * NK * 64;
+#pragma unroll
+    for (int s = 0; s < NK; ++s)
+      __builtin_amdgcn_global_load_lds(Vlo + vr * RW + 4 * s + q, scr + s * 64, 16, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll""", """    (void)ibase;
+    (void)loscr;
+#pragma unroll"""),
+        (TK, "      const tk_half8 bl = __builtin_bit_cast(tk_half8, scr[s * 64 + lane]);",
+         "      const tk_half8 bl = __builtin_bit_cast(tk_half8, tb[NBUF * VT * RW + ((4 * s + q) ^ swz)]);"),
+        (TK, "  const size_t tiles = 16 * nbuf * vt * (size_t)(kq / 8) +",
+         "  const size_t tiles = 2 * 16 * nbuf * vt * (size_t)(kq / 8) +"),
+        (TK, "                       4 * 16 * nw * (size_t)rg + 16 * nw * 64 * (size_t)nk;",
+         "                       4 * 16 * nw * (size_t)rg;"),
+        (TK, "  uint64_t* lk = reinterpret_cast<uint64_t*>(loscr + NW * NK * 64);  // 16-byte aligned",
+         "  uint64_t* lk = reinterpret_cast<uint64_t*>(loscr);  // 16-byte aligned"),
     ],
     # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
     "sweepc_nb4": [

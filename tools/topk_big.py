@@ -1,6 +1,7 @@
 """Dev: configs[4] top-10 / top-100 timing on configs[3]-shaped factors (2 ALS
 iterations from the seed), for the library ALS_HIP_LIB points at (with ALS_HIP_DEV=1).
-    python tools/topk_big.py [sample]"""
+    python tools/topk_big.py [sample]
+TOPK_SAVE=f.pt: save the results; TOPK_CMP=f.pt: print the agreement with saved ones."""
 import os
 import sys
 import time
@@ -27,9 +28,16 @@ def main():
     torch.cuda.synchronize()
     Q = core.U[:s].contiguous()
     lib = os.environ.get("ALS_HIP_LIB", "default")
+    res = {}
     for top in (10, 100):
-        E.topk_rows(Q, s, core.V, core.n_items, 128, top)
+        res[top] = E.topk_rows(Q, s, core.V, core.n_items, 128, top)
         torch.cuda.synchronize()
+        L = E._lib.lib()
+        cnt = hasattr(L, "als_dev_tk_counters")
+        if cnt:
+            import ctypes
+            buf = (ctypes.c_ulonglong * 8)()
+            L.als_dev_tk_counters(buf, 1)
         ts = []
         for _ in range(2):
             t0 = time.perf_counter()
@@ -37,6 +45,18 @@ def main():
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         print(f"{lib} top{top}: {1e3 * min(ts):.1f} ms  {s / min(ts) / 1e6:.3f} M recs/s", flush=True)
+        if cnt:
+            L.als_dev_tk_counters(buf, 1)
+            print(f"  counters per call: {[v // 2 for v in buf[:5]]}", flush=True)
+    if os.environ.get("TOPK_SAVE"):
+        torch.save({t: tuple(x.cpu() for x in r) for t, r in res.items()}, os.environ["TOPK_SAVE"])
+    if os.environ.get("TOPK_CMP"):
+        ref = torch.load(os.environ["TOPK_CMP"], weights_only=True)
+        for t, r in res.items():
+            i0, s0 = ref[t]
+            i1, s1 = (x.cpu() for x in r)
+            print(f"{lib} top{t}: index agreement {float((i0 == i1).float().mean()):.7f} "
+                  f"max|dscore| {float((s0 - s1).abs().max()):.3e}", flush=True)
 
 
 if __name__ == "__main__":

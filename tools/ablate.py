@@ -1,7 +1,7 @@
 """Dev tool: time the phases of the explicit light-row half-sweep kernels on the
 ML-25M-shaped synthetic data (tools/dev_ablate.hip: full / Gram only / solve only).
     python tools/ablate.py --build          (CPU: hipcc -> tools/libals_dev.so)
-    python tools/ablate.py [--rank 64|128]  (GPU box)
+    python tools/ablate.py [--rank 64|128] [--config big1b]  (GPU box; big1b: configs[3], items only)
 Prints ms per launch and ns per row for each mode on the item and the user side."""
 import ctypes
 import math
@@ -52,16 +52,24 @@ def main():
     P, F, I = ctypes.c_void_p, ctypes.c_float, ctypes.c_int
     L.dev_ablate.argtypes = [I, I, P, P, P, P, I, P, I, I, F, F, F, P, I, I, F, P, P, P]
     dev = torch.device("cuda", 0)
-    u, i, r = D.synthetic_config("ml25m", device=dev)
+    big = "--config" in sys.argv and sys.argv[sys.argv.index("--config") + 1] == "big1b"
+    u, i, r = D.big_config("big1b", device=dev) if big else D.synthetic_config("ml25m", device=dev)
     core = E.ALSCore(u, i, r, device=dev)
+    del u, i, r
+    torch.cuda.empty_cache()
     core.init_factors(k, seed=5)
     core.iterate(0.1)
     torch.cuda.synchronize()
     rcnt = torch.zeros(2, dtype=torch.int32, device=dev)
     names = {0: "full", 1: "gram only", 2: "solve only"}
-    for side, blk, Y, X in (("item", core.item_block, core.U, core.V),
-                            ("user", core.user_block, core.V, core.U)):
+    sides = (("item", core.item_block, core.U, core.V),
+             ("user", core.user_block, core.V, core.U))
+    for side, blk, Y, X in sides[:1] if big else sides:
         n = blk.n_light - blk.n_dual(k)  # the primal light rows (the dual tail has its own kernel)
+        lr = blk.light_rows[:n].long()
+        lnnz = int((blk.row_ptr[lr + 1] - blk.row_ptr[lr]).sum())
+        print(f"{side}: light {blk.n_light} (primal {n}, {lnnz} ratings), heavy {blk.n_heavy}, "
+              f"chunks {blk.n_chunks}, nnz {int(blk.row_ptr[-1])}", flush=True)
         X2 = torch.empty_like(X)
         rlist = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         Ysp, ey = split_table(Y, k, kp)

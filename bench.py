@@ -291,17 +291,17 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
 
 def topk_variant(k: int, top: int, n_q: int):
     """The kernel als_topk launches (csrc/topk.hip) and its grid in threads:
-    (<NK, row groups, list kind, 0>, grid)."""
+    (<NK, row groups, list kind>, grid)."""
     nk = max(32, kp_of(k)) // 32
     if top <= 16:  # two row groups from 4 x 256 x 256 query rows (topk_split_rg)
         rg, tr = (2 if n_q >= 4 * 256 * 256 else 1), (8 if top <= 8 else (12 if top <= 12 else 16))
     elif top <= 128:  # quad register lists, one row group
         rg, tr = 1, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
     else:
-        return f"topk_split_kernel<{nk},?,0,0>", None
+        return f"topk_split_kernel<{nk},?,0>", None
     nw = 8  # wavefronts per workgroup with register lists (tk_nw)
     grid = (n_q + 16 * nw * rg - 1) // (16 * nw * rg) * 64 * nw
-    return f"topk_split_kernel<{nk},{rg},{tr},0>", grid
+    return f"topk_split_kernel<{nk},{rg},{tr}>", grid
 
 
 def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int):

@@ -76,11 +76,11 @@ def test_phase_counters_combine_by_grid(bench, monkeypatch):
 
 
 @pytest.mark.parametrize("k,top,n_q,kern,grid", [
-    (128, 10, 10_000_000, "topk_split_kernel<4,2,12,0>", 39063 * 512),
-    (128, 100, 10_000_000, "topk_split_kernel<4,1,100,0>", 78125 * 512),
-    (64, 10, 162_541, "topk_split_kernel<2,1,12,0>", 1270 * 512),
-    (128, 10, 262_144, "topk_split_kernel<4,2,12,0>", 1024 * 512),
-    (128, 10, 262_143, "topk_split_kernel<4,1,12,0>", 2048 * 512),
-    (32, 20, 1000, "topk_split_kernel<1,1,32,0>", 8 * 512)])
+    (128, 10, 10_000_000, "topk_split_kernel<4,2,12>", 39063 * 512),
+    (128, 100, 10_000_000, "topk_split_kernel<4,1,100>", 78125 * 512),
+    (64, 10, 162_541, "topk_split_kernel<2,1,12>", 1270 * 512),
+    (128, 10, 262_144, "topk_split_kernel<4,2,12>", 1024 * 512),
+    (128, 10, 262_143, "topk_split_kernel<4,1,12>", 2048 * 512),
+    (32, 20, 1000, "topk_split_kernel<1,1,32>", 8 * 512)])
 def test_topk_variant_matches_launch_choice(bench, k, top, n_q, kern, grid):
     assert bench.topk_variant(k, top, n_q) == (kern, grid)

@@ -58,7 +58,8 @@ def main():
     else:
         u, i, r = D.synthetic_config("ml25m", device=dev)
         k, imp, alpha, warm = (64, False, 1.0, 3) if wl == "c1" else (128, True, 40.0, 3)
-    core = E.ALSCore(u, i, r, device=dev)
+    chunk = int(sys.argv[sys.argv.index("--chunk") + 1]) if "--chunk" in sys.argv else E.DEFAULT_CHUNK
+    core = E.ALSCore(u, i, r, device=dev, chunk=chunk)
     del u, i, r
     torch.cuda.empty_cache()
     core.init_factors(k, seed=5)
@@ -93,7 +94,8 @@ def main():
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
     core.check_status()
-    out = {"wl": wl, "lib": os.environ.get("ALS_HIP_LIB", "product"), "ms_per_iter": round(ms, 4)}
+    out = {"wl": wl, "lib": os.environ.get("ALS_HIP_LIB", "product"), "chunk": chunk,
+           "ms_per_iter": round(ms, 4)}
     if "--no-parity" not in sys.argv:
         out["max_row_err"] = parity(core, k, reg, imp, alpha)
     for key, lst in ev.items():

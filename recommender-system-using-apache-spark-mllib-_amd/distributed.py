@@ -338,12 +338,13 @@ class ShardedALS:
         """Pipeline the item half-sweep when the exchange it hides — U chunk C-1's
         all-gather, (W - 1) x a chunk's rows per rank — costs more than twice the
         partial-slot traffic it adds (every item row through the slot path: about three
-        passes over one slot per <= 2048-rating segment, two segments per row)."""
+        passes over one slot per <= DEFAULT_CHUNK-rating segment, two segments per row)."""
+        from . import engine as E
         if world < 2 or chunks < 2:
             return False
         ld = (rank + 3) // 4 * 4
         recv = (world - 1) * user_rows_per_chunk * ld * 4
-        segs = 2 * max(item_rows, 1) + item_nnz // 2048
+        segs = 2 * max(item_rows, 1) + item_nnz // E.DEFAULT_CHUNK
         cn = 1 if rank <= 16 else (2 if rank <= 32 else (4 if rank <= 64 else 8))
         slot = (cn * (cn + 1) // 2 * 4 + cn + 1) * 64 * 4
         t_ring = recv / (cls.RING_GBS * 1e9)

@@ -26,7 +26,7 @@ import torch
 from . import _lib
 from ._lib import check, ptr, stream_ptr
 
-DEFAULT_CHUNK = 2048  # ratings per heavy-row task
+DEFAULT_CHUNK = 4096  # ratings per heavy-row task (round 5: profiles/r05/ab_chunk*.jsonl)
 MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
 DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
 DUAL_MAX_RATINGS_64 = 32  # explicit, 32 < k <= 64: the same for rows this short

@@ -1,6 +1,6 @@
 """Parity at the benchmarked configurations, through the production path.
 
-Every call here uses the engine's defaults — DEFAULT_CHUNK (2048-rating tasks,
+Every call here uses the engine's defaults — DEFAULT_CHUNK (4096-rating tasks,
 fp32 accumulation inside a task, fp64 across a heavy row's chunks) and the
 bench's data generator — so the arithmetic checked is the arithmetic
 `bench.py` times (BASELINE.json configs[0]-[2]):
@@ -13,7 +13,7 @@ bench's data generator — so the arithmetic checked is the arithmetic
     data, implicit alpha = 40, rank 128): one item and one user half-sweep from
     identical source factors against the C restatement of Spark's dspr + dppsv
     (oracle/als_oracle.c), max per-row relative error <= 1e-4, reported by row
-    length so the 2048-rating fp32 tasks and the chunked heavy rows are visible;
+    length so the 4096-rating fp32 tasks and the chunked heavy rows are visible;
     K1's CSR at full size bit-exact against the numpy oracle.
   * top-10 of recommendForAllUsers for a 2,000-user sample at configs[1]
     against the fp64 oracle (identical except fp ties within 1e-5).

@@ -532,6 +532,7 @@ def timed_fit(core, workload, k, reg, imp, alpha, steps, warmup):
     and the event times of the primal and dual launches of each half-sweep
     -> (ms_per_iter, roofline of the primal kernel, dual view)."""
     core.init_factors(k, seed=5)
+    core.schedule_for(imp)  # the engine's heavy-row task length for this fit
     core.status.zero_()
     for _ in range(warmup):
         _iteration(core, k, reg, imp, alpha)

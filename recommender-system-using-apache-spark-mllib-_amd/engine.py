@@ -27,6 +27,16 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 
 DEFAULT_CHUNK = 4096  # ratings per heavy-row task (round 5: profiles/r05/ab_chunk*.jsonl)
+
+
+def chunk_for(rank: int, implicit: bool) -> int:
+    """Heavy-row task length of a half-sweep (ALSCore's default): a task's fp32 partial
+    slot grows as k^2, so explicit fits at rank > 64 take twice the ratings per slot.
+    Measured round 5 (profiles/r05/ab_chunk2.jsonl): configs[3] (k = 128, explicit) 8192
+    vs 4096 ratings 275.1 -> 270.6 ms/iter; at configs[1] (k = 64) 8192 took the longest
+    rows' error to 1.2e-6 and at configs[2] (implicit) the >2048-rating rows sit at
+    8e-7 with 4096 already, so those keep 4096."""
+    return 2 * DEFAULT_CHUNK if (rank > 64 and not implicit) else DEFAULT_CHUNK
 MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
 DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
 DUAL_MAX_RATINGS_64 = 32  # explicit, 32 < k <= 64: the same for rows this short
@@ -454,8 +464,12 @@ def make_engine(users, items, ratings, device=None):
 class ALSCore:
     """Ratings, id maps, both CSR sides and both factor matrices resident on one GPU."""
 
-    def __init__(self, users, items, ratings, device=None, chunk: int = DEFAULT_CHUNK):
+    def __init__(self, users, items, ratings, device=None, chunk: Optional[int] = None):
+        """chunk: ratings per heavy-row task; None = chunk_for(rank, implicit) of each
+        half-sweep (the blocks are rescheduled when a fit asks for another length)."""
         _lib.require_gpu()
+        self._auto_chunk = chunk is None
+        chunk = DEFAULT_CHUNK if chunk is None else chunk
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         # both CSR sides hold the same ratings: one rating scale for every half-sweep
@@ -495,6 +509,7 @@ class ALSCore:
             "cuda", torch.cuda.current_device())
         self.ws = Workspace(self.device)
         self.nnz = 0
+        self._auto_chunk = False
         self.user_block = self.item_block = None
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         U = _to_device(U, torch.float32, self.device)
@@ -551,12 +566,28 @@ class ALSCore:
                             dtype=torch.float32)
             self.U[:, :rank] = x / torch.linalg.vector_norm(x, dim=1, keepdim=True)
 
+    def schedule_for(self, implicit: bool) -> None:
+        """The default heavy-row task length for this fit's rank and feedback type (no-op
+        when the core was built with an explicit chunk)."""
+        if self._auto_chunk:
+            self.rechunk(chunk_for(self.rank, implicit))
+
+    def rechunk(self, chunk: int) -> None:
+        """Reschedule both sides for `chunk`-rating heavy-row tasks (same CSR)."""
+        for name in ("user_block", "item_block"):
+            b = getattr(self, name)
+            if b.chunk != chunk:
+                setattr(self, name, schedule_block(b.n_rows, b.nnz, b.row_ptr, b.col, b.val,
+                                                   self.ws, chunk))
+
     def half_sweep_items(self, reg, implicit=False, alpha=1.0):
+        self.schedule_for(implicit)
         yty = compute_yty(self.U, self.n_users, self.rank, self.ws) if implicit else None
         solve_half(self.item_block, self.U, self.V, self.rank, reg, implicit, alpha, yty,
                    self.status, self.ws)
 
     def half_sweep_users(self, reg, implicit=False, alpha=1.0):
+        self.schedule_for(implicit)
         yty = compute_yty(self.V, self.n_items, self.rank, self.ws) if implicit else None
         solve_half(self.user_block, self.V, self.U, self.rank, reg, implicit, alpha, yty,
                    self.status, self.ws)

@@ -94,7 +94,8 @@ def test_configs3_item_half_sweep(big):
     rows, heavy, deg = _sample(core.item_block, 50, 5000, 11)
     # the heavy head really is the many-hundred-chunk regime
     hdeg = deg[torch.as_tensor(heavy, device=DEV)]
-    assert int(hdeg.max()) > 500 * E.DEFAULT_CHUNK and int(hdeg.min()) > 100 * E.DEFAULT_CHUNK
+    ch = core.item_block.chunk
+    assert int(hdeg.max()) > 300 * ch and int(hdeg.min()) > 50 * ch
     report("configs3_item_chunks", {"n_chunks": core.item_block.n_chunks,
                                     "heaviest_50_ratings": [int(hdeg.min()), int(hdeg.max())]})
     _check_half(core, core.item_block, rows, U0, core.V, "configs3_item_half_sweep_by_row_length")
@@ -110,7 +111,7 @@ def test_configs3_user_half_sweep(big):
     rows, heavy, deg = _sample(core.user_block, 50, 20000, 12)
     # chunked heavy user rows, where the data has rows past the production chunk, are in
     # the sample (_sample takes the longest rows)
-    assert core.user_block.n_heavy > 0 or int(deg.max()) <= E.DEFAULT_CHUNK
+    assert core.user_block.n_heavy > 0 or int(deg.max()) <= core.user_block.chunk
     _check_half(core, core.user_block, rows, V0, core.U, "configs3_user_half_sweep_by_row_length")
 
 

@@ -1363,8 +1363,16 @@ __device__ __forceinline__ float sel_mask(float v, float w) {
 // pivots is checked by the caller from the spread test's minimum (dself_out), so the
 // returned minimum is not tracked here (+inf).  A 2 x 2-pivot form (8 sequential steps
 // instead of 16) measured slower: the same updates plus a 2 x 2 inverse per pair, and
-// the sweep is issue-bound, not chain-bound (A/B round 5, profiles/r05/ab_pair_pivots.jsonl).
-template <class Hook>
+// the sweep is issue-bound, not chain-bound (A/B round 5, profiles/r05/ab_pair_pivots.jsonl)
+// — at two or more waves per SIMD.  LA (the one-wave-per-SIMD W1 kernels, NB = 8): the
+// next pivot row's broadcast is issued one pivot earlier, before the current pivot's
+// update, and brought up to date on the copy by one more DPP fmac (the same fp32
+// operation as on its register, so the results are bit-identical): the ds_bpermute
+// latency leaves the pivot chain for one VALU more per pivot.  A/B round 5
+// (profiles/r05/ab_lookahead.jsonl): configs[3] W1 user rows 96.6 -> 95.2 ms, 271.9 -> 270.1
+// ms/iter; slower
+// where other waves hide the chain (k <= 64: user launch +0.7 %, dual rows +2.5 %).
+template <bool LA = false, class Hook>
 __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
   // Bv was just written by the matrix cores (the pivot block's Schur update) and is
   // read below by inline DPP asm, which the hazard recognizer does not see: the XDL
@@ -1374,6 +1382,8 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
   float dmin = 3.0e38f;
   float dself = 1.f;
   float rowp = rowgroup_bcast<0>(B[0]);
+  float pre = 0.f;  // LA: the next pivot row's broadcast copy
+  if constexpr (LA) pre = rowgroup_bcast<0>(B[1]);  // row 1 before pivot 0
   float d = bcast16<0>(rowp);
   float rd = rcp_t(d);
   float f = rowp * rd;
@@ -1382,21 +1392,36 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
     constexpr int p = decltype(pc)::value;
     constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
     asm volatile("s_nop 1" ::: "memory");
-    // the register holding row p+1 first: then pivot p+1's row is final
-    fmac_bcast16<p>(B[rn], nf);
     float dn = 0.f, rdn = 0.f, fn = 0.f, nfn = 0.f;
-    if constexpr (p + 1 < 16) {
-      constexpr int qn = (p + 1) >> 2;
-      const float rown = rowgroup_bcast<qn>(B[rn]);
-      dn = bcast16<p + 1>(rown);
-      rdn = rcp_t(dn);
-      fn = rown * rdn;
-      nfn = sel_lane16_n<p + 1>(0.f, fn);
+    if constexpr (LA) {
+      if constexpr (p + 1 < 16) {  // row p+1 after pivot p, on its broadcast copy
+        fmac_bcast16<p>(pre, nf);
+        dn = bcast16<p + 1>(pre);
+        rdn = rcp_t(dn);
+        fn = pre * rdn;
+        nfn = sel_lane16_n<p + 1>(0.f, fn);
+      }
+      static_for<4>([&](auto rc) { fmac_bcast16<p>(B[decltype(rc)::value], nf); });
+      if constexpr (p + 2 < 16) {  // row p+2 after pivots <= p: consumed by pivot p+1
+        constexpr int q2 = (p + 2) / 4, r2 = (p + 2) % 4;
+        pre = rowgroup_bcast<q2>(B[r2]);
+      }
+    } else {
+      // the register holding row p+1 first: then pivot p+1's row is final
+      fmac_bcast16<p>(B[rn], nf);
+      if constexpr (p + 1 < 16) {
+        constexpr int qn = (p + 1) >> 2;
+        const float rown = rowgroup_bcast<qn>(B[rn]);
+        dn = bcast16<p + 1>(rown);
+        rdn = rcp_t(dn);
+        fn = rown * rdn;
+        nfn = sel_lane16_n<p + 1>(0.f, fn);
+      }
+      static_for<4>([&](auto rc) {
+        constexpr int r = decltype(rc)::value;
+        if constexpr (r != rn) fmac_bcast16<p>(B[r], nf);
+      });
     }
-    static_for<4>([&](auto rc) {
-      constexpr int r = decltype(rc)::value;
-      if constexpr (r != rn) fmac_bcast16<p>(B[r], nf);
-    });
     // row p (row group qp): f off the pivot, -1 on it (scaled by 1/d at the end)
     B[rp] = sel_mask<0xFFFFull << (16 * qp)>(sel_lane16<p>(-1.f, f), B[rp]);
     dself = sel_lane16<p>(d, dself);
@@ -1657,7 +1682,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
       // swept in the C layout: Gm comes out where the MFMAs read it
       Gm = A[w1_tile<NB>(K, K)];
       float ds;
-      dmin = fminf(dmin, sweep16c(Gm, hook, ds));
+      dmin = fminf(dmin, sweep16c<NB == 8>(Gm, hook, ds));
       track_pivot(ds, m * NB + K < k);
       const float bK = K == 0 ? bcol[0] : reduce_rows4(bcol[K]);  // partials -> b_K[m]
       if (q == 0) vec[m] = bK;

@@ -170,6 +170,62 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
         (TK, "  uint64_t* lk = reinterpret_cast<uint64_t*>(loscr + NW * NK * 64);  // 16-byte aligned",
          "  uint64_t* lk = reinterpret_cast<uint64_t*>(loscr);  // 16-byte aligned"),
     ],
+    # sweep16c: the next pivot row's broadcast issued one pivot earlier (before the
+    # current pivot's update) and brought up to date on the copy by one more DPP fmac
+    # (the same fp32 operation as on its register): the ds_bpermute latency leaves the
+    # pivot chain, one VALU more per pivot
+    "lookahead": [
+        (GS, """  float rowp = rowgroup_bcast<0>(B[0]);
+  float d = bcast16<0>(rowp);
+  float rd = rcp_t(d);
+  float f = rowp * rd;
+  float nf = sel_lane16_n<0>(0.f, f);
+  static_for<16>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    constexpr int qp = p >> 2, rp = p & 3, rn = (p + 1) & 3;
+    asm volatile("s_nop 1" ::: "memory");
+    // the register holding row p+1 first: then pivot p+1's row is final
+    fmac_bcast16<p>(B[rn], nf);
+    float dn = 0.f, rdn = 0.f, fn = 0.f, nfn = 0.f;
+    if constexpr (p + 1 < 16) {
+      constexpr int qn = (p + 1) >> 2;
+      const float rown = rowgroup_bcast<qn>(B[rn]);
+      dn = bcast16<p + 1>(rown);
+      rdn = rcp_t(dn);
+      fn = rown * rdn;
+      nfn = sel_lane16_n<p + 1>(0.f, fn);
+    }
+    static_for<4>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      if constexpr (r != rn) fmac_bcast16<p>(B[r], nf);
+    });""", """  float rowp = rowgroup_bcast<0>(B[0]);
+  float pre = rowgroup_bcast<0>(B[1]);  // row 1 before pivot 0
+  float d = bcast16<0>(rowp);
+  float rd = rcp_t(d);
+  float f = rowp * rd;
+  float nf = sel_lane16_n<0>(0.f, f);
+  static_for<16>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    constexpr int qp = p >> 2, rp = p & 3;
+    asm volatile("s_nop 1" ::: "memory");
+    float dn = 0.f, rdn = 0.f, fn = 0.f, nfn = 0.f;
+    if constexpr (p + 1 < 16) {
+      // row p+1 after pivot p, on its broadcast copy
+      fmac_bcast16<p>(pre, nf);
+      dn = bcast16<p + 1>(pre);
+      rdn = rcp_t(dn);
+      fn = pre * rdn;
+      nfn = sel_lane16_n<p + 1>(0.f, fn);
+    }
+    static_for<4>([&](auto rc) {
+      constexpr int r = decltype(rc)::value;
+      fmac_bcast16<p>(B[r], nf);
+    });
+    if constexpr (p + 2 < 16) {  // row p+2 after pivots <= p: consumed by pivot p+1
+      constexpr int q2 = (p + 2) / 4, r2 = (p + 2) % 4;
+      pre = rowgroup_bcast<q2>(B[r2]);
+    }"""),
+    ],
     # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
     "sweepc_nb4": [
         (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = NB == 4;"),

@@ -1369,9 +1369,9 @@ __device__ __forceinline__ float sel_mask(float v, float w) {
 // update, and brought up to date on the copy by one more DPP fmac (the same fp32
 // operation as on its register, so the results are bit-identical): the ds_bpermute
 // latency leaves the pivot chain for one VALU more per pivot.  A/B round 5
-// (profiles/r05/ab_lookahead.jsonl): configs[3] W1 user rows 96.6 -> 95.2 ms, 271.9 -> 270.1
-// ms/iter; slower
-// where other waves hide the chain (k <= 64: user launch +0.7 %, dual rows +2.5 %).
+// (profiles/r05/ab_lookahead.jsonl): configs[3] W1 user rows 96.6 -> 95.2 ms, 271.9 ->
+// 270.1 ms/iter; slower where other waves hide the chain (k <= 64: user launch +0.7 %,
+// dual rows +2.5 %).
 template <bool LA = false, class Hook>
 __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
   // Bv was just written by the matrix cores (the pivot block's Schur update) and is

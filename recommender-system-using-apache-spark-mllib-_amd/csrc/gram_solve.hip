@@ -1480,7 +1480,8 @@ constexpr bool kW1SplitSchur = NB == 8;
 // `profiles/r05/ab_sweepc_nb.jsonl`, configs[3] 287.4 -> 280.1 ms/iter (explicit
 // rank-128 user launch 101.5 -> 96.3 ms, dual systems 65.6 -> 64.7 ms), configs[1]
 // 2.043 -> 2.032.  In the split-Schur form (implicit rank-128 light rows, heavy-row
-// solves) it is slower: configs[2] 9.32 -> 10.99 ms/iter (user launch 5.48 -> 6.66).
+// solves) it is slower: configs[2] 9.32 -> 10.99 ms/iter (user launch 5.48 -> 6.66), and
+// still with the pivot lookahead of the W1 sweep: 9.12 -> 10.75 (ab_sweepc_split_lookahead.jsonl).
 template <int NB, bool SPLIT>
 constexpr bool kSweepC = !SPLIT;
 // Measured round 4 (A/B at configs[1] / configs[3]): the split form in the explicit

@@ -226,6 +226,14 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
       pre = rowgroup_bcast<q2>(B[r2]);
     }"""),
     ],
+    # timing bound (wrong results): the split-in-registers Gram (implicit) gathers only
+    # rows 0..63 of Y (cache-hot): how much of the implicit launches is gather latency
+    "hotgather": [
+        (GS, "    TS::load_clamped(Y + (int64_t)(ids[j] >= 0 ? ids[j] : 0) * ld, s.y[j], d0, ld);",
+         "    TS::load_clamped(Y + (int64_t)(ids[j] >= 0 ? (ids[j] & 63) : 0) * ld, s.y[j], d0, ld);"),
+        (GS, "  if ((threadIdx.x & 63) == 0) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);",
+         "  if (false) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);"),
+    ],
     # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
     "sweepc_nb4": [
         (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = NB == 4;"),

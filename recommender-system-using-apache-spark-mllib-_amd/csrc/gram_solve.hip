@@ -50,7 +50,10 @@ namespace als {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
-constexpr int kRescueGrid = 256;     // workgroups walking the rescue list (rescue64_kernel)
+// workgroups walking the rescue list (rescue64_kernel).  64, not 256: an empty list (the
+// usual case) still costs one finished-block atomic per workgroup on one word; configs[1]
+// LAUNCH2 + RESCUE phases 3 us shorter per half-sweep (profiles/r05/ab_rescue_grid.jsonl).
+constexpr int kRescueGrid = 64;
 // Largest LDL^T pivot spread (max / min pivot of the real dims, a lower bound on
 // cond(A)) the fp32 solve keeps: beyond it the row is re-solved in fp64.  Regularised
 // rating data (lambda 0.1) spread far less (pivots lie in [lambda_min, lambda_max] and

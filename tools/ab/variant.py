@@ -234,6 +234,10 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
         (GS, "  if ((threadIdx.x & 63) == 0) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);",
          "  if (false) {\n    const unsigned i = atomicAdd(rl.cnt, 1u);"),
     ],
+    # rescue launch with 64 workgroups (its finished-block counter: 64 atomics, not 256)
+    "rescue64wg": [
+        (GS, "constexpr int kRescueGrid = 256;", "constexpr int kRescueGrid = 64;"),
+    ],
     # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
     "sweepc_nb4": [
         (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = NB == 4;"),

@@ -447,7 +447,7 @@ __host__ __device__ constexpr int tk_vt(int nk, int topr) {
 // Tile buffers in LDS: the one scored and the next one landing.  (Three, i.e. two
 // tiles in flight, measured slower: top-100 203 vs 193 ms at 128-row tiles — a refined
 // block's vmcnt(0) then also waits for the later tile's pieces.)
-__host__ __device__ constexpr int tk_nbuf(int topr) { return topr == 0 ? 2 : 2; }
+__host__ __device__ constexpr int tk_nbuf(int topr) { return (void)topr, 2; }
 
 // Tile-row swizzle: uint4 column c of tile row r sits at c ^ sw(r), sw(r) = (r >> 1) & 3
 // at RW = 4 (NK = 1), r & (RW - 1) at RW = 8, 16: the ds_read_b128 lane groups of gfx950

@@ -931,3 +931,28 @@ def test_topk_nan_factor_row(rank, top):
                            - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
         np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
     del S
+
+
+@pytest.mark.parametrize("rank,implicit,fixed", [(64, False, None), (128, False, None),
+                                                 (128, True, None), (128, False, 1024)])
+def test_task_length_follows_the_fit(rank, implicit, fixed):
+    """ALSCore(chunk=None) schedules each half-sweep with engine.chunk_for(rank, implicit)
+    (8192 explicit at rank > 64, else 4096); an explicit chunk stays fixed.  The factors
+    are the same fp64-checked solve either way: one item half-sweep against the oracle."""
+    from oracle import c_oracle as C
+    u, i, r = planted(300, 40, density=0.9, seed=21, heavy_items=(0, 1))
+    core = E.ALSCore(u, i, r, device=DEV, chunk=fixed)
+    core.init_factors(rank, seed=2)
+    U0 = core.U[:, :rank].cpu().numpy()
+    core.half_sweep_items(0.1, implicit=implicit, alpha=3.0)
+    torch.cuda.synchronize()
+    core.check_status()
+    want = fixed if fixed is not None else E.chunk_for(rank, implicit)
+    assert core.item_block.chunk == want and core.user_block.chunk == want
+    b = core.item_block
+    ref, st = C.half_sweep(b.row_ptr.cpu().numpy(), b.col.cpu().numpy(), b.val.cpu().numpy(), U0,
+                           0.1, implicit=implicit, alpha=3.0)
+    assert not st.any()
+    err = rel_row_err(core.V[:, :rank].cpu().numpy(), ref)
+    report(f"task_length[rank={rank},imp={int(implicit)},chunk={want}]", err)
+    assert err < 1e-5, err

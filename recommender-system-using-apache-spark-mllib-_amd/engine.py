@@ -39,6 +39,7 @@ def chunk_for(rank: int, implicit: bool) -> int:
     return 2 * DEFAULT_CHUNK if (rank > 64 and not implicit) else DEFAULT_CHUNK
 MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
 DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
+# (round 5, configs[3]: limit 64 / 80 / 96 -> 288.9 / 275.8 / 267.2 ms/iter, profiles/r05/ab_dual_limit.jsonl)
 DUAL_MAX_RATINGS_64 = 32  # explicit, 32 < k <= 64: the same for rows this short
 
 # als_solve_half phase bits (include/als_hip.h ALS_PHASE_*)

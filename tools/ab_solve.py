@@ -60,6 +60,8 @@ def main():
         k, imp, alpha, warm = (64, False, 1.0, 3) if wl == "c1" else (128, True, 40.0, 3)
     chunk = int(sys.argv[sys.argv.index("--chunk") + 1]) if "--chunk" in sys.argv else E.DEFAULT_CHUNK
     core = E.ALSCore(u, i, r, device=dev, chunk=chunk)
+    if "--dual" in sys.argv:  # a lower dual-path row-length limit (rank > 64), <= the built 96
+        E.DUAL_MAX_RATINGS = int(sys.argv[sys.argv.index("--dual") + 1])
     del u, i, r
     torch.cuda.empty_cache()
     core.init_factors(k, seed=5)
@@ -95,6 +97,7 @@ def main():
     ms = 1e3 * (time.perf_counter() - t0) / steps
     core.check_status()
     out = {"wl": wl, "lib": os.environ.get("ALS_HIP_LIB", "product"), "chunk": chunk,
+           "dual_max": E.DUAL_MAX_RATINGS,
            "ms_per_iter": round(ms, 4)}
     if "--no-parity" not in sys.argv:
         out["max_row_err"] = parity(core, k, reg, imp, alpha)

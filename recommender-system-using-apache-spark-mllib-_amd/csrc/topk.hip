@@ -440,9 +440,11 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // LDS to the lists.
 // (Round 5, LDS-DMA staging, configs[4] 262,144-user sample: 192-row tiles at rank >
 // 64 vs 128: top-10 91.5 -> 89.4 ms, top-100 193.5 -> 189.5 ms; 256 rows do not fit
-// the LDS beside the lo scratch and the score blocks.)
+// the LDS beside the lo scratch and the score blocks.  At rank <= 64, 384 / nk rows vs
+// 256 / nk, all 162,541 ML-25M-shaped users: top-10 3.85 -> 3.60 ms, top-100 20.8 ->
+// 19.7 ms, profiles/r05/ab_topk_small_tiles.txt.)
 __host__ __device__ constexpr int tk_vt(int nk, int topr) {
-  return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 256 / nk);
+  return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 384 / nk);
 }
 // Tile buffers in LDS: the one scored and the next one landing.  (Three, i.e. two
 // tiles in flight, measured slower: top-100 203 vs 193 ms at 128-row tiles — a refined

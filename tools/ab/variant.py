@@ -238,6 +238,15 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
     "rescue64wg": [
         (GS, "constexpr int kRescueGrid = 256;", "constexpr int kRescueGrid = 64;"),
     ],
+    # top-k: 1.5x larger tiles at rank <= 64 (192 rows at k <= 64, 384 at k <= 32)
+    "tk_vt_small": [
+        (TK, "return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 384 / nk);",
+         "return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 384 / nk);"),
+    ],
+    "tk_vt_small2": [
+        (TK, "return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 384 / nk);",
+         "return topr == 0 ? 64 / nk : (nk == 4 ? 192 : 512 / nk);"),
+    ],
     # the C-layout sweep only for NB = 4 (the round-4 choice) / in every elimination
     "sweepc_nb4": [
         (GS, "constexpr bool kSweepC = !SPLIT;", "constexpr bool kSweepC = NB == 4;"),

@@ -16,21 +16,24 @@ from als_mi355x import datasets as D, engine as E  # noqa: E402
 
 
 def main():
-    s = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
+    ml = len(sys.argv) > 1 and sys.argv[1] == "ml25m"  # configs[1] shape, rank 64, all users
+    s = 0 if ml else (int(sys.argv[1]) if len(sys.argv) > 1 else 262144)
     dev = torch.device("cuda", 0)
-    u, i, r = D.big_config("big1b", device=dev)
+    k = 64 if ml else 128
+    u, i, r = D.synthetic_config("ml25m", device=dev) if ml else D.big_config("big1b", device=dev)
     core = E.ALSCore(u, i, r, device=dev)
     del u, i, r
     torch.cuda.empty_cache()
-    core.init_factors(128, seed=5)
+    core.init_factors(k, seed=5)
     for _ in range(2):
         core.iterate(0.1)
     torch.cuda.synchronize()
+    s = s or core.n_users
     Q = core.U[:s].contiguous()
     lib = os.environ.get("ALS_HIP_LIB", "default")
     res = {}
     for top in (10, 100):
-        res[top] = E.topk_rows(Q, s, core.V, core.n_items, 128, top)
+        res[top] = E.topk_rows(Q, s, core.V, core.n_items, k, top)
         torch.cuda.synchronize()
         L = E._lib.lib()
         cnt = hasattr(L, "als_dev_tk_counters")
@@ -41,7 +44,7 @@ def main():
         ts = []
         for _ in range(2):
             t0 = time.perf_counter()
-            E.topk_rows(Q, s, core.V, core.n_items, 128, top)
+            E.topk_rows(Q, s, core.V, core.n_items, k, top)
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
         print(f"{lib} top{top}: {1e3 * min(ts):.1f} ms  {s / min(ts) / 1e6:.3f} M recs/s", flush=True)

@@ -31,12 +31,12 @@ DEFAULT_CHUNK = 4096  # ratings per heavy-row task (round 5: profiles/r05/ab_chu
 
 def chunk_for(rank: int, implicit: bool) -> int:
     """Heavy-row task length of a half-sweep (ALSCore's default): a task's fp32 partial
-    slot grows as k^2, so explicit fits at rank > 64 take twice the ratings per slot.
-    Measured round 5 (profiles/r05/ab_chunk2.jsonl): configs[3] (k = 128, explicit) 8192
-    vs 4096 ratings 275.1 -> 270.6 ms/iter; at configs[1] (k = 64) 8192 took the longest
-    rows' error to 1.2e-6 and at configs[2] (implicit) the >2048-rating rows sit at
-    8e-7 with 4096 already, so those keep 4096."""
-    return 2 * DEFAULT_CHUNK if (rank > 64 and not implicit) else DEFAULT_CHUNK
+    slot grows as k^2, so explicit fits at rank > 64 take four times the ratings per slot.
+    Measured round 5 (profiles/r05/ab_chunk2.jsonl, ab_chunk3.jsonl): configs[3] (k = 128,
+    explicit) 4096 / 8192 / 16384 ratings 275.1 / 270.6 / 266.3 ms/iter; at configs[1]
+    (k = 64) 8192 took the longest rows' error to 1.2e-6 and at configs[2] (implicit) the
+    >2048-rating rows sit at 8e-7 with 4096 already, so those keep 4096."""
+    return 4 * DEFAULT_CHUNK if (rank > 64 and not implicit) else DEFAULT_CHUNK
 MAX_RANK = 128       # k <= 64: gram_solve_kernel; 64 < k <= 128: W1 (one wavefront per system)
 DUAL_MAX_RATINGS = 96  # explicit, 64 < k <= 128: rows this short go through the n x n dual
 # (round 5, configs[3]: limit 64 / 80 / 96 -> 288.9 / 275.8 / 267.2 ms/iter, profiles/r05/ab_dual_limit.jsonl)

@@ -69,7 +69,9 @@ def test_configs3_sharded_one_rank_matches_engine(monkeypatch):
         monkeypatch.setattr(Dm.dist, name, counted(name))
     try:
         u, i, r = D.big_config("big1b", device=DEV)
-        core = E.ALSCore(u, i, r, device=DEV)
+        # the sharded engine's task length (its blocks are scheduled once, at setup): the
+        # same per-row arithmetic on both sides
+        core = E.ALSCore(u, i, r, device=DEV, chunk=E.DEFAULT_CHUNK)
         sh = Dm.ShardedALS(u, i, r, device=DEV)  # auto chunks, as bench.py configs3
         del u, i, r
         torch.cuda.empty_cache()

@@ -30,7 +30,7 @@ gram + solve launch of each half-sweep (ALS_PHASE_LAUNCH1), timed alone with HIP
 events on the launching stream; the dual-path launch of the short rows
 (ALS_PHASE_DUAL) is timed and reported beside it (`dual`).  `frac` = algorithmic
 bytes per launch / event time / 8 TB/s; the same over the kernel-trace average of
-the PMC profiling runs (`frac_pmc_profile`: tools/gpu_pmc_r04.sh, `bench.py --only W
+the PMC profiling runs (`frac_pmc_profile`: tools/gpu_pmc.sh, `bench.py --only W
 --steps 3`, a different and shorter run than this one); the PMC traffic / counter DRAM fraction / busy fractions
 / limiter of that workload's own profiled launches (profiles/pmc_summary.json,
 keyed by workload, kernel and grid size).  `cpu_baseline`: the C port of Spark's
@@ -126,7 +126,7 @@ def _pmc_doc():
 
 def load_pmc(workload: str, kernel: str, grid=None):
     """Per-launch rocprofv3 counters of `kernel` in the committed profile of `workload`
-    (tools/gpu_pmc_r03.sh -> tools/pmc_fold.py; format 2: workloads -> kernel ->
+    (tools/gpu_pmc.sh, tools/gpu_pmc_topk.sh -> tools/pmc_fold.py; format 2: workloads -> kernel ->
     all-dispatch averages + by_grid[grid threads]).  grid: the launch's grid size in
     threads, which tells the item launch of a half-sweep from the user launch."""
     ent = _pmc_doc().get("workloads", {}).get(workload, {}).get(kernel.replace(" ", ""))

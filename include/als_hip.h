@@ -74,8 +74,8 @@ int als_csr_build(const int32_t* row_ids, const int32_t* row_map,
 
 /* Work schedule for one CSR side: rows with <= chunk ratings ("light") are
  * solved one wavefront each, longest first; heavier rows are split into
- * chunk-sized tasks whose fp64 partial normal equations are reduced in a
- * second launch.  Two-step: count (device int32[3] = n_light, n_heavy,
+ * chunk-sized tasks whose partial normal equations (fp32 sums within a task,
+ * stored as those fp32 values) are summed in fp64 and solved in a second launch.  Two-step: count (device int32[3] = n_light, n_heavy,
  * n_chunks) then build into caller buffers sized from those counts. */
 size_t als_schedule_workspace_bytes(int32_t n_rows);
 int als_schedule_count(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
@@ -100,7 +100,8 @@ int als_schedule_build(const int64_t* row_ptr, int32_t n_rows, int32_t chunk,
  * max |rating|.  Explicit: Y_src is split once per call into a table in the
  * workspace ((n_src + 1) x k_pad words) and the rhs runs on the matrix cores too;
  * implicit: the split follows the per-rating confidence weight, in registers.
- * fp32 sums within a task of <= 2048 ratings, fp64 across a heavy row's tasks;
+ * fp32 sums within a task (the schedule's chunk: engine.chunk_for picks 4096
+ * ratings, 16384 for explicit fits at k > 64), fp64 across a heavy row's tasks;
  * solved by a square-root-free block LDL^T (the solution of Spark's Cholesky
  * dppsv) in fp32, stored fp32 into X_dst[row*ld ..].  k <= 128, n_src < 2^31.
  * Parity bar: 1e-4 relative per row against the fp64 restatement of Spark's

@@ -165,3 +165,74 @@ def test_library_override_needs_the_dev_flag(tmp_path):
                            env=dict(base, **extra), capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr[-2000:]
         assert p.stdout.strip().splitlines()[-1] == want
+
+
+_C_TYPES = {"int32_t": _lib.I32, "int64_t": _lib.I64, "float": _lib.F32, "size_t": _lib.SZ,
+            "int": ctypes.c_int}
+
+
+def _header_signatures():
+    """name -> ctypes argtypes, parsed from the prototypes of include/als_hip.h
+    (every pointer is a c_void_p on the Python side; `void` = no parameters)."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(als_[a-z_0-9]+)\s*\(([^)]*)\)\s*;", src):
+        params = [p.strip() for p in m.group(2).split(",") if p.strip() not in ("", "void")]
+        types = []
+        for p in params:
+            if "*" in p:
+                types.append(_lib.P)
+            else:
+                base = p.replace("const ", "").split()[0]
+                types.append(_C_TYPES[base])
+        out[m.group(1)] = types
+    return out
+
+
+def test_header_parameter_types_match_the_binding():
+    """Every prototype's parameter list (count and C type) is what _lib.SIGNATURES binds."""
+    hdr = _header_signatures()
+    assert sorted(hdr) == sorted(_lib.SIGNATURES)
+    for name, (_, args) in _lib.SIGNATURES.items():
+        assert hdr[name] == args, name
+
+
+def _integration_stub():
+    """Run the INTEGRATION.md section-2 ctypes stub against a recording stand-in for
+    CDLL (no library is loaded) and return (recorded argtypes, the call's arg count)."""
+    import ast
+    import types
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = text[text.index("## 2."):]
+    code = re.search(r"```python\n(.*?)```", sec, flags=re.S).group(1)
+
+    class Rec(types.SimpleNamespace):
+        def __getattr__(self, name):
+            f = types.SimpleNamespace()
+            setattr(self, name, f)
+            return f
+
+    rec = Rec()
+    fake_ctypes = types.SimpleNamespace(**{k: getattr(ctypes, k) for k in dir(ctypes)
+                                           if not k.startswith("_")})
+    fake_ctypes.CDLL = lambda path: rec
+    body = code.replace("import ctypes, torch", "pass")
+    ns = {"ctypes": fake_ctypes, "torch": None}
+    exec(compile(body, "INTEGRATION.md", "exec"), ns)
+    n_call = None
+    for node in ast.walk(ast.parse(body)):
+        if (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute)
+                and node.func.attr == "als_solve_half"):
+            n_call = len(node.args)
+    return rec, n_call
+
+
+def test_integration_stub_matches_the_abi():
+    """The stand-alone binding a maintainer would copy from INTEGRATION.md binds the
+    same argtypes as _lib.py (ABI 6: 29 for als_solve_half) and calls it with that many."""
+    rec, n_call = _integration_stub()
+    res, args = _lib.SIGNATURES["als_solve_half"]
+    assert rec.als_solve_half.argtypes == args
+    assert rec.als_solve_half.restype == res
+    assert n_call == len(args) == len(_header_signatures()["als_solve_half"])
+    assert rec.als_solve_workspace_bytes.argtypes == _lib.SIGNATURES["als_solve_workspace_bytes"][1]

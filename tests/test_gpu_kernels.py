@@ -937,7 +937,7 @@ def test_topk_nan_factor_row(rank, top):
                                                  (128, True, None), (128, False, 1024)])
 def test_task_length_follows_the_fit(rank, implicit, fixed):
     """ALSCore(chunk=None) schedules each half-sweep with engine.chunk_for(rank, implicit)
-    (8192 explicit at rank > 64, else 4096); an explicit chunk stays fixed.  The factors
+    (16384 explicit at rank > 64, else 4096); an explicit chunk stays fixed.  The factors
     are the same fp64-checked solve either way: one item half-sweep against the oracle."""
     from oracle import c_oracle as C
     u, i, r = planted(300, 40, density=0.9, seed=21, heavy_items=(0, 1))

@@ -1,5 +1,5 @@
 """Dev A/B timing of half-sweep variants (NOT the bench): one workload, the library
-named by ALS_HIP_LIB (a tools/ab/build_solve.sh build) or the product one.
+named by ALS_HIP_LIB (a tools/ab/variant.py build) or the product one.
     ALS_HIP_DEV=1 ALS_HIP_LIB=tools/ab/libals_x.so python tools/ab_solve.py c1|c2|c3 [steps]
 Prints one JSON line: ms per iteration and the event time of each phase launch."""
 import json
@@ -14,6 +14,12 @@ import _pkgload  # noqa: E402
 
 _pkgload.load()
 from als_mi355x import datasets as D, engine as E  # noqa: E402
+from als_mi355x import _lib as _L  # noqa: E402
+
+
+def _lib_loaded():
+    """The library actually loaded (ALS_HIP_LIB counts only with ALS_HIP_DEV=1)."""
+    return _L.LIB_PATH
 
 
 def parity(core, k, reg, imp, alpha, n_rows=3000):
@@ -96,7 +102,7 @@ def main():
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
     core.check_status()
-    out = {"wl": wl, "lib": os.environ.get("ALS_HIP_LIB", "product"), "chunk": chunk,
+    out = {"wl": wl, "lib": _lib_loaded(), "chunk": chunk,
            "dual_max": E.DUAL_MAX_RATINGS,
            "ms_per_iter": round(ms, 4)}
     if "--no-parity" not in sys.argv:

@@ -1,7 +1,7 @@
 """Dev A/B timing of recommendForAll variants (NOT the bench): the configs[3] factors
 after two ALS iterations (10M users x 1M items, rank 128), top-10 and top-100 for a
 262,144-user prefix (or all users with --all), with the library named by ALS_HIP_LIB (+ ALS_HIP_DEV=1; a
-tools/ab/build_solve.sh build) or the product one; a 64-user sample is checked against
+tools/ab/variant.py build) or the product one; a 64-user sample is checked against
 the fp64 oracle (identical except fp64 ties within 1e-5).
     ALS_HIP_LIB=tools/ab/libals_x.so python tools/ab_topk.py [--all]"""
 import json
@@ -16,6 +16,12 @@ import _pkgload  # noqa: E402
 
 _pkgload.load()
 from als_mi355x import datasets as D, engine as E  # noqa: E402
+from als_mi355x import _lib as _L  # noqa: E402
+
+
+def _lib_loaded():
+    """The library actually loaded (ALS_HIP_LIB counts only with ALS_HIP_DEV=1)."""
+    return _L.LIB_PATH
 from oracle import als_oracle as O  # noqa: E402
 
 
@@ -31,7 +37,7 @@ def main():
         core.iterate(0.1)
     torch.cuda.synchronize()
     n_q = core.n_users if "--all" in sys.argv else 262_144
-    out = {"lib": os.environ.get("ALS_HIP_LIB", "product"), "n_q": n_q}
+    out = {"lib": _lib_loaded(), "n_q": n_q}
     V = core.V[:, :k].cpu().numpy()
     rows = np.arange(0, n_q, n_q // 64)[:64]
     for top in (10, 100):

@@ -1,4 +1,4 @@
-"""Fold rocprofv3 outputs of tools/profile.sh into profiles/:
+"""Fold rocprofv3 outputs of tools/gpu_pmc.sh / tools/gpu_pmc_topk.sh into profiles/:
   profiles/<tag>_kernel_stats.csv   (rocprofv3 --kernel-trace --stats summary, copied)
   profiles/<tag>_pmc.json           (per-kernel FETCH_SIZE / WRITE_SIZE per launch)
   profiles/pmc_summary.json         (what bench.py reads for roofline.traffic)

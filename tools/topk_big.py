@@ -30,7 +30,8 @@ def main():
     torch.cuda.synchronize()
     s = s or core.n_users
     Q = core.U[:s].contiguous()
-    lib = os.environ.get("ALS_HIP_LIB", "default")
+    from als_mi355x import _lib as _L
+    lib = _L.LIB_PATH  # the library actually loaded (ALS_HIP_LIB counts only with ALS_HIP_DEV=1)
     res = {}
     for top in (10, 100):
         res[top] = E.topk_rows(Q, s, core.V, core.n_items, k, top)

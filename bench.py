@@ -733,7 +733,7 @@ def big_distributed(args, dev, rank, world):
     torch.cuda.synchronize()
     t_gen = time.perf_counter() - t0
     t0 = time.perf_counter()
-    sh = ShardedALS(u, i, r, device=dev, chunks=args.chunks)
+    sh = ShardedALS(u, i, r, device=dev, chunks=args.chunks, **_sharded_opts(args))
     torch.cuda.synchronize()
     t_build = time.perf_counter() - t0
     del u, i, r
@@ -748,7 +748,7 @@ def big_distributed(args, dev, rank, world):
            "ratings_per_s": sh.nnz / (t / steps), "ms_per_iter": 1e3 * t / steps,
            "steps": steps, "warmup": 1, "datagen_s": t_gen, "build_s": t_build,
            "scaling": "strong", "n_gpus": world, "chunks": sh.users.chunks,
-           "exchange": sh.exchange_stats(k)}
+           "exchange": dict(sh.exchange_stats(k), mode=sh.exchange, pipelined=sh.pipeline)}
     # configs[4]: each rank scores its own users (every chunk of its range) against the
     # replicated V; time = max over ranks
     Vd = sh._dense(False)
@@ -775,6 +775,13 @@ def big_distributed(args, dev, rank, world):
     return res, c4
 
 
+def _sharded_opts(args) -> dict:
+    """--exchange / --pipeline -> ShardedALS arguments (defaults: RCCL ring all-gather,
+    no pipelined item half-sweep)."""
+    pipe = {"off": None, "on": True, "auto": "auto"}[args.pipeline]
+    return {"exchange": args.exchange, "pipeline": pipe}
+
+
 def run_distributed(args):
     from als_mi355x.distributed import ShardedALS
     for k_, v_ in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"),
@@ -786,12 +793,12 @@ def run_distributed(args):
     dist.init_process_group("nccl", device_id=dev)
     rank, world = dist.get_rank(), dist.get_world_size()
     u, i, r = D.synthetic_config(args.config, device=dev, shard=rank)
-    sh = ShardedALS(u, i, r, device=dev, chunks=args.chunks)
+    sh = ShardedALS(u, i, r, device=dev, chunks=args.chunks, **_sharded_opts(args))
     del u, i, r
     k = args.rank
     sh.init_factors(k, seed=5)
     t_total = _timed_iterations(sh, args.reg, args.warmup, args.steps, dev)
-    ex = sh.exchange_stats(k)
+    ex = dict(sh.exchange_stats(k), mode=sh.exchange, pipelined=sh.pipeline)
     out = None
     if rank == 0:
         out = {
@@ -864,6 +871,10 @@ def main():
                     help="timed iterations of configs[3] (at most --steps)")
     ap.add_argument("--chunks", type=int, default=None,
                     help="row chunks per rank for the overlapped all-gathers (N>1)")
+    ap.add_argument("--exchange", choices=("ring", "peers"), default="ring",
+                    help="N > 1: factor exchange (RCCL ring all-gather or batched P2P to all peers)")
+    ap.add_argument("--pipeline", choices=("off", "on", "auto"), default="off",
+                    help="N > 1: the pipelined item half-sweep (auto: the exchange model)")
     ap.add_argument("--only", choices=("c1", "c2", "c3", "c4"), default=None,
                     help="profiling runs: only this workload (c4 fits c3 untimed first)")
     ap.add_argument("--force-dist", action="store_true",

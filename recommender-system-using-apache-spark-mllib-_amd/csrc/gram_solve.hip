@@ -3006,10 +3006,11 @@ __global__ __launch_bounds__(kRescueThreads) void rescue64_kernel(
   }
   // the list is consumed: the last block to finish (every block read the count before
   // its increment) empties it for the next LAUNCH1 of this workspace.  rl.cnt[1] is
-  // the finished-block counter (zeroed with the count by the prep, reset here).
+  // the finished-block counter (zeroed with the count by the prep, reset here).  No
+  // fence: a block's read of the count returned before its increment was issued (the
+  // loop bound depends on it), and nothing else in this launch reads what it wrote.
   __syncthreads();
   if (tid == 0) {
-    __threadfence();
     if (atomicAdd(rl.cnt + 1, 1u) == gridDim.x - 1) {
       rl.cnt[0] = 0u;
       rl.cnt[1] = 0u;
@@ -3185,9 +3186,10 @@ static size_t slot_bytes(int32_t k, int32_t n_chunks) {
 size_t als_solve_workspace_bytes(int32_t k, int32_t n_chunks, int64_t n_src, int32_t n_rows) {
   // From the front: 256 B of scale words (max |Y_src|, max |rating|, rescue count) |
   // C-layout YtY (W1 implicit) | partial slots of the heavy-row chunks (n_chunks,
-  // counted from slot 0: chunk_slot0 + the call's chunks) | rescue list (n_rows).
+  // counted from slot 0: chunk_slot0 + the call's chunks).
   // From the back: the split table ((n_src + 1) x k_pad words, explicit), ending at
-  // the workspace's end (256-B aligned; + 256 B of slack for that alignment).  Calls
+  // the workspace's end (256-B aligned; + 256 B of slack for that alignment), and
+  // right below it the rescue list (n_rows).  Calls
   // that share one PREP (row chunks of a half-sweep: same Y_src, any n_chunks / n_rows)
   // find the table at the same place, and the two calls of a two-segment half-sweep
   // (different n_src) find the early partial slots at the same place.
@@ -3242,10 +3244,13 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
   const float* scal = reinterpret_cast<const float*>(scal_u);
   float* ytyC = reinterpret_cast<float*>(static_cast<char*>(ws) + 256);
   double* slots = reinterpret_cast<double*>(static_cast<char*>(ws) + 256 + ytyc_bytes(k));
-  int32_t* rescue_list = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(slots) +
-                                                    slot_bytes(k, n_slots));
   uint32_t* Ysp = reinterpret_cast<uint32_t*>(
       static_cast<char*>(ws) + ((ws_bytes - solve_table_bytes(k, n_src)) & ~(size_t)255));
+  // the rescue list right below the split table (not after this call's slots: blocks
+  // sharing one workspace with disjoint slot ranges must not see one call's list land
+  // on another block's partial slots; the size check keeps it above every slot)
+  int32_t* rescue_list = reinterpret_cast<int32_t*>(
+      reinterpret_cast<char*>(Ysp) - align_up(sizeof(int32_t) * (size_t)(n_rows > 0 ? n_rows : 0)));
   unsigned* rescue_cnt = scal_u + 2;
   const RescueList rl{rescue_cnt, rescue_list, (unsigned)(n_light + n_heavy)};
   // the rescue list (count at scale word 2, the rescue launch's finished-block counter

@@ -47,30 +47,53 @@ from .engine import id_offset
 
 
 class HipKernels:
-    """The product kernels (libals_hip.so) behind the interface ShardedALS uses."""
+    """The product kernels (libals_hip.so) behind the interface ShardedALS uses.
+
+    chunk: ratings per heavy-row task; None = the single-GPU engine's choice per fit
+    (engine.chunk_for(rank, implicit): 16384 for explicit fits at rank > 64, else 4096),
+    applied by ShardedALS rescheduling its blocks when a fit asks for another length."""
 
     def __init__(self, device, chunk: Optional[int] = None):
         from . import engine as E
         self.E = E
         self.device = torch.device(device)
         self.ws = E.Workspace(self.device)
+        self.auto_chunk = chunk is None
         self.chunk = chunk or E.DEFAULT_CHUNK
         self.max_chunks = 0  # heavy-row chunks of the largest block: one workspace layout
         self.max_rows = 0    # rows of the largest block (rescue list)
-        self.split_ws = {}   # per-block workspaces of the pipelined (two-segment) item side
+        # the pipelined (two-segment) item side: one workspace for every item chunk, the
+        # chunks' slots in disjoint ranges, one Y prep per part (engine.solve_half_split)
+        self.split_ws = E.Workspace(self.device)
+        self.split_slots = 0
+        self.split_rows = 0
+
+    def chunk_for(self, rank: int, implicit: bool) -> int:
+        return self.E.chunk_for(rank, implicit) if self.auto_chunk else self.chunk
+
+    def reschedule(self, block, chunk: int):
+        """The same CSR block with `chunk`-rating heavy-row tasks."""
+        blk = self.E.schedule_block(block.n_rows, block.nnz, block.row_ptr, block.col, block.val,
+                                    self.ws, chunk)
+        self.max_chunks = max(self.max_chunks, blk.n_chunks)
+        self.max_rows = max(self.max_rows, blk.n_light + blk.n_heavy)
+        return blk
+
+    def block_chunk(self, block) -> int:
+        return block.chunk
 
     def index_build(self, ids: torch.Tensor, id_space: int):
         idx = self.E.build_index(ids.to(self.device, torch.int32).contiguous(), id_space, self.ws)
         return idx.map, idx.uniq, idx.n
 
     def build_block(self, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor,
-                    n_rows: int, n_cols: int):
+                    n_rows: int, n_cols: int, chunk: Optional[int] = None):
         ident_r = torch.arange(max(n_rows, 1), dtype=torch.int32, device=self.device)
         ident_c = torch.arange(max(n_cols, 1), dtype=torch.int32, device=self.device)
         ri = self.E.IdIndex(ident_r, ident_r, n_rows)
         ci = self.E.IdIndex(ident_c, ident_c, n_cols)
         blk = self.E.build_block(rows.contiguous(), ri, cols.contiguous(), ci,
-                                 vals.contiguous(), self.ws, self.chunk)
+                                 vals.contiguous(), self.ws, chunk or self.chunk)
         self.max_chunks = max(self.max_chunks, blk.n_chunks)
         self.max_rows = max(self.max_rows, blk.n_light + blk.n_heavy)
         return blk
@@ -86,17 +109,24 @@ class HipKernels:
                      phases=E.PHASE_ALL if first else E.PHASE_ALL & ~E.PHASE_PREP,
                      ws_chunks=self.max_chunks, ws_rows=self.max_rows)
 
-    def split_schedule(self, block, seg, n_src_early: int):
-        """Two-segment schedule of an item block (pipelined item half-sweep)."""
-        return self.E.split_schedule(block, seg, n_src_early, self.chunk)
+    def split_schedule(self, block, seg, n_src_early: int, slot_base: int = 0):
+        """Two-segment schedule of an item block (pipelined item half-sweep), its slots
+        numbered from slot_base (the item chunks share one workspace)."""
+        sched = self.E.split_schedule(block, seg, n_src_early, block.chunk, slot_base)
+        self.split_slots = max(self.split_slots, sched.n_slots)
+        self.split_rows = max(self.split_rows, block.n_rows)
+        return sched
+
+    def split_slot_end(self, sched) -> int:
+        return sched.n_slots
 
     def solve_split(self, block, sched, part, Y, X, rank, reg, implicit, alpha, yty, status,
-                    key):
-        """One part ("early" / "late") of a two-segment half-sweep; `key` names the block's
-        own workspace (its early partials must stay in place until its late call)."""
-        ws = self.split_ws.setdefault(key, self.E.Workspace(self.device))
+                    first: bool):
+        """One part ("early" / "late") of a two-segment half-sweep on the shared item
+        workspace; first: the first item chunk of this part (it preps Y for them all)."""
         self.E.solve_half_split(block, sched, part, Y, X, rank, reg, implicit, alpha, yty,
-                                status, ws)
+                                status, self.split_ws, prep=first, ws_slots=self.split_slots,
+                                ws_rows=self.split_rows)
 
     def predict(self, u_keys, i_keys, umap, imap, U, V, rank) -> torch.Tensor:
         E = self.E
@@ -261,7 +291,21 @@ class ShardedALS:
     """ALS with users and items sharded over the ranks of `group`."""
 
     def __init__(self, users, items, ratings, device=None, group=None, kernels=None,
-                 chunks: Optional[int] = None, pipeline: Optional[bool] = None):
+                 chunks: Optional[int] = None, pipeline=None, exchange: str = "ring"):
+        """pipeline: the pipelined item half-sweep (below).  None / False: off (the
+        default until an A/B on a multi-GPU node shows it pays: no such node has been
+        available to this build); True: on; "auto": on when the exchange model
+        (pipeline_pays) says so at the fit's rank.
+        exchange: how a solved factor chunk reaches every rank — "ring": RCCL's
+        all_gather_into_tensor; "peers": one batched isend / irecv per peer (every rank
+        sends its chunk to all W - 1 peers at once, so all xGMI links carry traffic
+        instead of the ring's one in / one out link per step; unmeasured on a
+        multi-GPU node)."""
+        if exchange not in ("ring", "peers"):
+            raise ValueError(f"exchange must be 'ring' or 'peers', got {exchange!r}")
+        if pipeline not in (None, False, True, "auto"):
+            raise ValueError(f"pipeline must be None, False, True or 'auto', got {pipeline!r}")
+        self.exchange = exchange
         self.group = group
         self.proc = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -310,16 +354,20 @@ class ShardedALS:
         self.user_blocks = self._blocks(self.users, ru, rc, rv, self.items)
         ri_, rc_, rv_ = self._route(self.items.owner_of(idn), i_pad, u_pad, r)
         self.item_rows = self._local_rows(self.items)
-        # pipelined item half-sweep (default with several ranks and >= 2 user chunks):
-        # each item row's ratings are split into the users of chunks 0..C-2 (early) and
-        # of chunk C-1 (late), so the early partial normal equations are formed while
-        # the last user chunk's all-gather is still in flight (_pipelined_items)
-        if pipeline is None:
-            pipeline = self._pipeline_pays(ri_, rc_)
-        self.pipeline = bool(pipeline) and self.users.chunks >= 2
+        self.item_nnz = int(ri_.numel())
+        # pipelined item half-sweep: each item row's ratings are split into the users of
+        # chunks 0..C-2 (early) and of chunk C-1 (late), so the early partial normal
+        # equations are formed while the last user chunk's all-gather is still in
+        # flight (_pipelined_items).  The item blocks are built early-first whenever it
+        # may run; whether it does is settled per fit (init_factors: "auto" asks the
+        # exchange model at the fit's rank).
+        self._pipeline_arg = pipeline
+        # (True also at one rank, where it only exercises the two-segment kernels)
+        can_split = bool(pipeline) and self.users.chunks >= 2
+        self.pipeline = False
         self.item_split = None
-        self.item_blocks = self._blocks(self.items, ri_, rc_, rv_, self.users,
-                                        split=self.pipeline)
+        self._item_segs = None
+        self.item_blocks = self._blocks(self.items, ri_, rc_, rv_, self.users, split=can_split)
         self._pending_u = []  # async all-gathers of U chunks not yet waited for
         self._yty_u = None    # YtY of the final U (implicit, pipelined): formed early
         self.status = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -333,32 +381,91 @@ class ShardedALS:
     HBM_GBS = 5000.0
 
     @classmethod
-    def pipeline_pays(cls, world: int, chunks: int, user_rows_per_chunk: int,
-                      item_rows: int, item_nnz: int, rank: int = 128) -> bool:
-        """Pipeline the item half-sweep when the exchange it hides — U chunk C-1's
-        all-gather, (W - 1) x a chunk's rows per rank — costs more than twice the
-        partial-slot traffic it adds (every item row through the slot path: about three
-        passes over one slot per <= DEFAULT_CHUNK-rating segment, two segments per row)."""
+    def pipeline_cost(cls, world: int, chunks: int, user_rows_per_chunk: int, item_rows: int,
+                      item_nnz: int, rank: int, item_chunks: int = 1,
+                      chunk: Optional[int] = None) -> dict:
+        """The exchange model of the pipelining choice, per item half-sweep (seconds):
+        hidden = U chunk C-1's all-gather, (W - 1) x a chunk's rows per rank, which the
+        early item partials hide; added = the partial-slot traffic (every item row
+        through the slot path: about three passes over one slot per <= chunk-rating
+        segment, two segments per row) plus the extra Y prep (one over the arrived prefix
+        of U for the early part, beside the one every half-sweep does: read U, write
+        its split table)."""
         from . import engine as E
+        chunk = chunk or E.DEFAULT_CHUNK
+        ld = (rank + 3) // 4 * 4
+        kp = 16 * (1 if rank <= 16 else (2 if rank <= 32 else (4 if rank <= 64 else 8)))
+        cn = kp // 16
+        recv = (world - 1) * user_rows_per_chunk * ld * 4
+        segs = 2 * max(item_rows, 1) + item_nnz // chunk
+        slot = (cn * (cn + 1) // 2 * 4 + cn + 1) * 64 * 4
+        n_u = world * chunks * user_rows_per_chunk
+        prep = n_u * (ld + kp) * 4 * (chunks - 1) / max(chunks, 1)
+        return {"hidden_s": recv / (cls.RING_GBS * 1e9),
+                "added_s": (3 * segs * slot + prep) / (cls.HBM_GBS * 1e9)}
+
+    @classmethod
+    def pipeline_pays(cls, world: int, chunks: int, user_rows_per_chunk: int,
+                      item_rows: int, item_nnz: int, rank: int = 128, item_chunks: int = 1,
+                      chunk: Optional[int] = None) -> bool:
+        """Pipeline the item half-sweep when the exchange it hides costs more than twice
+        what it adds (pipeline_cost)."""
         if world < 2 or chunks < 2:
             return False
-        ld = (rank + 3) // 4 * 4
-        recv = (world - 1) * user_rows_per_chunk * ld * 4
-        segs = 2 * max(item_rows, 1) + item_nnz // E.DEFAULT_CHUNK
-        cn = 1 if rank <= 16 else (2 if rank <= 32 else (4 if rank <= 64 else 8))
-        slot = (cn * (cn + 1) // 2 * 4 + cn + 1) * 64 * 4
-        t_ring = recv / (cls.RING_GBS * 1e9)
-        t_slots = 3 * segs * slot / (cls.HBM_GBS * 1e9)
-        return t_slots < 0.5 * t_ring
+        c = cls.pipeline_cost(world, chunks, user_rows_per_chunk, item_rows, item_nnz, rank,
+                              item_chunks, chunk)
+        return c["added_s"] < 0.5 * c["hidden_s"]
 
-    def _pipeline_pays(self, rows_pad, cols_pad) -> bool:
-        """pipeline_pays for this rank's item rows at rank 128 (the factor rank is not
-        known yet), agreed by every rank (MIN)."""
+    def _pipeline_pays(self, rank: int, implicit: bool = False) -> bool:
+        """pipeline_pays for this rank's item rows at the fit's rank and task length,
+        agreed by every rank (MIN)."""
+        chunk = self.K.chunk_for(rank, implicit) if hasattr(self.K, "chunk_for") else None
         ok = self.pipeline_pays(self.world, self.users.chunks, self.users.rows_per_chunk,
-                                self._local_rows(self.items), int(rows_pad.numel()))
+                                self.item_rows, self.item_nnz, rank, self.items.chunks, chunk)
         flag = torch.tensor([1 if ok else 0], dtype=torch.int64, device=self.device)
         all_reduce_capped(flag, "pipeline choice", dist.ReduceOp.MIN, self.group)
         return bool(int(flag))
+
+    def _settle_pipeline(self, rank: int, implicit: bool = False) -> None:
+        """Whether this fit pipelines the item half-sweep (the item blocks were built
+        early-first at setup when it may)."""
+        arg = self._pipeline_arg
+        if self._item_segs is None or not arg:
+            self.pipeline = False
+        elif arg == "auto":
+            self.pipeline = self._pipeline_pays(rank, implicit)
+        else:
+            self.pipeline = True
+
+    def _schedule_for(self, implicit: bool) -> None:
+        """The heavy-row task length of this fit (HipKernels.chunk_for: the single-GPU
+        engine's choice) for every block; the pipelined item side's two-segment
+        schedules are rebuilt with it."""
+        if not hasattr(self.K, "reschedule") or self.rank == 0:
+            return
+        chunk = self.K.chunk_for(self.rank, implicit)
+        blocks = [b for b in self.user_blocks + self.item_blocks if b is not None]
+        if all(self.K.block_chunk(b) == chunk for b in blocks):
+            return
+        self.user_blocks = [None if b is None else self.K.reschedule(b, chunk)
+                            for b in self.user_blocks]
+        self.item_blocks = [None if b is None else self.K.reschedule(b, chunk)
+                            for b in self.item_blocks]
+        if self._item_segs is not None:
+            self._split_schedules()
+
+    def _split_schedules(self) -> None:
+        """Two-segment schedules of the item blocks, slot ranges disjoint (one shared
+        workspace, one Y prep per part)."""
+        n_src_early = (self.users.chunks - 1) * self.world * self.users.rows_per_chunk
+        self.item_split = []
+        base = 0
+        for blk, seg in zip(self.item_blocks, self._item_segs):
+            sched = None
+            if blk is not None:
+                sched = self.K.split_schedule(blk, seg, n_src_early, base)
+                base = self.K.split_slot_end(sched) if hasattr(self.K, "split_slot_end") else 0
+            self.item_split.append(sched)
     def _auto_chunks(self, u_space: int, i_space: int) -> int:
         """4 row chunks when a rank's share of the larger id space reaches 1M rows
         (the all-gather then moves >= 256 MB per rank at rank 64); 2 from 4 ranks on
@@ -418,8 +525,7 @@ class ShardedALS:
             order = torch.argsort(late.to(torch.int8), stable=True)
             rows_pad, cols_pad, vals, late = rows_pad[order], cols_pad[order], vals[order], \
                 late[order]
-            self.item_split = []
-        n_src_early = (other.chunks - 1) * W * other.rows_per_chunk
+            self._item_segs = []
         p = rows_pad.long()
         c = p // (W * rpc)
         j = (p % rpc).to(torch.int32)
@@ -431,12 +537,14 @@ class ShardedALS:
                                      W * other.rows_per_rank) if n_c > 0 else None
             out.append(blk)
             if split:
-                sched = None
+                seg = None
                 if blk is not None:
                     ne = torch.bincount(j[sel & ~late].long(), minlength=n_c)
                     seg = self._row_starts(blk, n_c) + ne.to(torch.int64)
-                    sched = self.K.split_schedule(blk, seg, n_src_early)
-                self.item_split.append(sched)
+                self._item_segs.append(seg)
+        if split:
+            self.item_blocks = out
+            self._split_schedules()
         return out
 
     def _row_starts(self, blk, n_rows: int) -> torch.Tensor:
@@ -503,6 +611,7 @@ class ShardedALS:
         self._drain()
         self._yty_u = None
         self.rank = rank
+        self._settle_pipeline(rank)
         self._dense_cache = {}
         ld = self.K.ld(rank)
         dev = self.device
@@ -530,8 +639,11 @@ class ShardedALS:
         del x
         full = self.U_full.view(us.chunks, -1, ld)
         _guard(full[0].numel() * full.element_size(), "factor all_gather")
+        works = []
         for c in range(us.chunks):
-            dist.all_gather_into_tensor(full[c], self.U_loc[c], group=self.group)
+            works.extend(self._exchange(full[c], self.U_loc[c]))
+        for w in works:
+            w.wait()
 
     def _yty(self, loc: torch.Tensor):
         # local rows of every chunk (padding rows are zero and add nothing), then all_reduce
@@ -556,14 +668,36 @@ class ShardedALS:
                 first = False
             if before_last is not None and c == len(blocks) - 1:
                 before_last()
-            works.append(dist.all_gather_into_tensor(Xf[c], X_loc[c], group=self.group,
-                                                     async_op=True))
+            works.extend(self._exchange(Xf[c], X_loc[c]))
         self._dense_cache = {}
         if not wait:
             return works
         for w in works:
             w.wait()
         return []
+
+    def _exchange(self, full_c: torch.Tensor, loc_c: torch.Tensor) -> list:
+        """Start the exchange of this rank's solved chunk loc_c into full_c ([world, rows,
+        ld]: every rank's chunk c) on every rank; returns the pending works.
+        "ring": one all_gather_into_tensor (RCCL's ring over xGMI: W - 1 steps, each
+        rank's one in / one out link busy per step).  "peers": one batched group of
+        isend / irecv, this rank's chunk to each of the W - 1 peers and theirs into
+        full_c[peer] (every link at once), the own chunk copied locally."""
+        _guard(loc_c.numel() * loc_c.element_size() * self.world, "factor exchange")
+        if self.exchange == "ring" or self.world == 1:
+            return [dist.all_gather_into_tensor(full_c, loc_c, group=self.group, async_op=True)]
+        fv = full_c.view(self.world, *loc_c.shape)
+        fv[self.proc].copy_(loc_c)
+        ops = []
+        for step in range(1, self.world):  # peers in a rotated order: no hot spot at rank 0
+            to, frm = (self.proc + step) % self.world, (self.proc - step) % self.world
+            ops.append(dist.P2POp(dist.isend, loc_c, self._peer(to), group=self.group))
+            ops.append(dist.P2POp(dist.irecv, fv[frm], self._peer(frm), group=self.group))
+        return dist.batch_isend_irecv(ops)
+
+    def _peer(self, r: int) -> int:
+        """Global rank of process r of self.group."""
+        return r if self.group is None else dist.get_global_rank(self.group, r)
 
     def _drain(self) -> None:
         """Wait for the U all-gathers a pipelined user half-sweep left in flight."""
@@ -579,22 +713,25 @@ class ShardedALS:
         pend = self._pending_u
         for w in pend[:-1]:
             w.wait()
+        first = True
         for c, blk in enumerate(self.item_blocks):
             if blk is not None:
                 self.K.solve_split(blk, self.item_split[c], "early", self.U_full, self.V_loc[c],
-                                   self.rank, reg, implicit, alpha, yty, self.status, ("i", c))
+                                   self.rank, reg, implicit, alpha, yty, self.status, first)
+                first = False
         for w in pend[-1:]:
             w.wait()
         self._pending_u = []
         Vf = self.V_full.view(self.V_loc.shape[0], -1, self.V_full.shape[1])
         _guard(Vf[0].numel() * Vf.element_size(), "factor all_gather")
         works = []
+        first = True
         for c, blk in enumerate(self.item_blocks):
             if blk is not None:
                 self.K.solve_split(blk, self.item_split[c], "late", self.U_full, self.V_loc[c],
-                                   self.rank, reg, implicit, alpha, yty, self.status, ("i", c))
-            works.append(dist.all_gather_into_tensor(Vf[c], self.V_loc[c], group=self.group,
-                                                     async_op=True))
+                                   self.rank, reg, implicit, alpha, yty, self.status, first)
+                first = False
+            works.extend(self._exchange(Vf[c], self.V_loc[c]))
         for w in works:
             w.wait()
         self._dense_cache = {}
@@ -627,6 +764,7 @@ class ShardedALS:
             before_last=before_last, wait=not self.pipeline)
 
     def iterate(self, reg, implicit=False, alpha=1.0):
+        self._schedule_for(implicit)
         self.half_sweep_items(reg, implicit, alpha)
         self.half_sweep_users(reg, implicit, alpha)
 
@@ -656,6 +794,7 @@ class ShardedALS:
         if Uc is not None:
             U0, U0_global = None, Uc
         self.init_factors(rank, seed, U0, U0_global)
+        self._settle_pipeline(rank, implicit)
         if Vc is not None:
             self._set_dense(False, Vc)
         self.status.zero_()
@@ -679,6 +818,8 @@ class ShardedALS:
         full[pad, :self.rank] = F
         loc.copy_(full.view(loc.shape[0], self.world, -1, full.shape[1])[:, self.proc])
         self._dense_cache = {}
+        if user_side:  # the YtY a pipelined user half-sweep formed for the old U
+            self._yty_u = None
 
     def fingerprint(self) -> dict:
         """ALSCore.fingerprint over the ratings of all ranks."""

@@ -311,17 +311,21 @@ class SplitSchedule:
     source rows lie in the first n_src_early rows of Y (already gathered) — then
     [seg[r], row_ptr[r+1]) (the late segment: the source chunk still arriving).  Each
     segment is cut into <= chunk-rating tasks; every row goes through the heavy-row
-    path (fp32 task partials summed per row in fp64, then solved), early slots first."""
+    path (fp32 task partials summed per row in fp64, then solved), early slots first.
+    Slots are numbered from slot_base (several blocks sharing one workspace and one Y
+    prep keep disjoint slot ranges: ShardedALS's item chunks)."""
     n_src_early: int
     rows: torch.Tensor          # int32 [n]: every row of the block, ascending
     slot_begin: torch.Tensor    # int32 [n+1]: early slots of row r
     slot_begin2: torch.Tensor   # int32 [n+1]: late slots of row r (after all early ones)
     early: tuple                # (chunk_row, chunk_begin, chunk_end, n_tasks)
     late: tuple
+    slot_base: int = 0          # first slot of this block's range in the workspace
 
     @property
     def n_slots(self) -> int:
-        return self.early[3] + self.late[3]
+        """Slots of the workspace up to this block's last (slot_base included)."""
+        return self.slot_base + self.early[3] + self.late[3]
 
 
 def _segment_tasks(row_ids, begin, end, chunk: int, dev):
@@ -344,9 +348,9 @@ def _segment_tasks(row_ids, begin, end, chunk: int, dev):
 
 
 def split_schedule(block: RatingBlock, seg: torch.Tensor, n_src_early: int,
-                   chunk: int = DEFAULT_CHUNK) -> SplitSchedule:
+                   chunk: int = DEFAULT_CHUNK, slot_base: int = 0) -> SplitSchedule:
     """The two-segment schedule of `block` (its rows' ratings ordered early-first, seg[r]
-    = end of row r's early segment)."""
+    = end of row r's early segment), its slots numbered from slot_base."""
     dev = block.row_ptr.device
     n = block.n_rows
     rp = block.row_ptr
@@ -354,32 +358,43 @@ def split_schedule(block: RatingBlock, seg: torch.Tensor, n_src_early: int,
     rows = torch.arange(max(n, 1), dtype=torch.int32, device=dev)
     sb1, early = _segment_tasks(rows[:n], rp[:-1], seg, chunk, dev)
     sb2, late = _segment_tasks(rows[:n], seg, rp[1:], chunk, dev)
-    sb2 = sb2 + early[3]
+    sb1 = sb1 + slot_base
+    sb2 = sb2 + early[3] + slot_base
     return SplitSchedule(int(n_src_early), rows, sb1.to(torch.int32).contiguous(),
-                         sb2.to(torch.int32).contiguous(), early, late)
+                         sb2.to(torch.int32).contiguous(), early, late, int(slot_base))
 
 
 def solve_half_split(block: RatingBlock, sched: SplitSchedule, part: str, Y: torch.Tensor,
                      X: torch.Tensor, rank: int, reg: float, implicit: bool, alpha: float,
-                     yty: Optional[torch.Tensor], status: torch.Tensor, ws: Workspace) -> None:
+                     yty: Optional[torch.Tensor], status: torch.Tensor, ws: Workspace,
+                     prep: bool = True, ws_slots: Optional[int] = None,
+                     ws_rows: Optional[int] = None) -> None:
     """One half of a two-segment half-sweep (ABI 6).  part "early": the early segments'
     task partials from the first sched.n_src_early rows of Y (PREP over that prefix,
     RSCALE, LAUNCH1), while the rest of Y may still be arriving; "late": the late
     segments' partials from all of Y, then every row's slots summed and solved
     (LAUNCH2) and the rescue (RESCUE, over the row's full ratings).  Both calls on
-    the same workspace, early first, in stream order."""
+    the same workspace, early first, in stream order.  Both pass slot_begin2 (it marks
+    the schedule two-segment: no heavy row is solved before its late partials).
+    prep=False: Y's prep for this part was done by an earlier call on this workspace
+    (blocks sharing one workspace with disjoint slot ranges, sized by ws_slots /
+    ws_rows for the largest: all early calls first, then all late ones)."""
     L = _lib.lib()
     n = block.n_rows
-    w = ws.get(L.als_solve_workspace_bytes(rank, sched.n_slots, Y.shape[0], n))
+    w = ws.get(L.als_solve_workspace_bytes(rank, max(sched.n_slots, ws_slots or 0), Y.shape[0],
+                                           max(n, ws_rows or 0)))
     if part == "early":
         crow, cb, ce, nt = sched.early
-        ph, slot0, sb2, n_src = PHASE_PREP | PHASE_RSCALE | PHASE_LAUNCH1, 0, None, sched.n_src_early
+        ph, slot0, n_src = PHASE_PREP | PHASE_RSCALE | PHASE_LAUNCH1, sched.slot_base, sched.n_src_early
     elif part == "late":
         crow, cb, ce, nt = sched.late
         ph = PHASE_PREP | PHASE_RSCALE | PHASE_LAUNCH1 | PHASE_LAUNCH2 | PHASE_RESCUE
-        slot0, sb2, n_src = sched.early[3], sched.slot_begin2, Y.shape[0]
+        slot0, n_src = sched.slot_base + sched.early[3], Y.shape[0]
     else:
         raise ValueError(f"part must be 'early' or 'late', got {part!r}")
+    if not prep:
+        ph &= ~PHASE_PREP
+    sb2 = sched.slot_begin2
     check(L.als_solve_half(ptr(block.row_ptr), ptr(block.col), ptr(block.val),
                            ptr(block.light_rows), 0, 0, ptr(sched.rows), ptr(sched.slot_begin), n,
                            ptr(crow), ptr(cb), ptr(ce), nt, ptr(sb2), slot0,

@@ -46,11 +46,11 @@ class OracleKernels:
         x = self.O.solve(A, b, ne, reg, None if yty is None else yty.numpy())
         X[:n, :rank] = torch.as_tensor(x)
 
-    def split_schedule(self, block, seg, n_src_early):
+    def split_schedule(self, block, seg, n_src_early, slot_base=0):
         return {"seg": np.asarray(seg.cpu()), "n_src_early": int(n_src_early), "part": None}
 
     def solve_split(self, block, sched, part, Y, X, rank, reg, implicit, alpha, yty, status,
-                    key):
+                    first):
         """Two-segment half-sweep: the early part's normal equations from the early
         rating segments with every source row past n_src_early poisoned (NaN: the early
         part must never read the chunk still in flight), the late part's added in fp64."""
@@ -110,7 +110,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, implicit, chunks, out_dir, pipeline=None):
+def _worker(rank, world, port, implicit, chunks, out_dir, pipeline=None, exchange="ring"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, root)
@@ -127,7 +127,7 @@ def _worker(rank, world, port, implicit, chunks, out_dir, pipeline=None):
     # arbitrary (non-aligned) input sharding: interleaved ratings
     sel = np.arange(len(u)) % world == rank
     K = ShardedALS(u[sel], i[sel], r[sel], device="cpu", kernels=OracleKernels(), chunks=chunks,
-                   pipeline=pipeline)
+                   pipeline=pipeline, exchange=exchange)
     from oracle import als_oracle as O
     n_users = len(np.unique(u))
     U0 = O.initialize(n_users, 6, seed=2)
@@ -214,23 +214,30 @@ def test_sharded_serving_matches_oracle(tmp_path, world):
     np.testing.assert_array_equal(d["sids"][0], uids[ref_u[0]])
 
 
-@pytest.mark.parametrize("implicit,chunks,world,pipeline",
-                         [(False, None, 2, None), (True, None, 2, None), (False, 3, 2, True),
-                          (True, 3, 2, True), (False, 3, 2, None), (True, 3, 2, None),
-                          (False, 2, 8, True), (True, 2, 8, True), (True, None, 8, None)])
-def test_sharded_als_matches_single_process(tmp_path, implicit, chunks, world, pipeline):
-    """chunks=3: the [C, world, rows] layout with async per-chunk all-gathers; with
-    several ranks and >= 2 chunks the item half-sweep is pipelined (default): the item
-    rows' early partials (users of chunks 0..C-2, every later source row poisoned with
-    NaN in the oracle kernels) are formed while the last user chunk's all-gather is in
-    flight, the late ones after; pipeline=False runs the plain chunked exchange.  world
-    8: the target world size of BASELINE configs[3] (8 x MI355X), every rank a range of
-    ~15 users and ~11 items, the full 3-iteration fit against the single-process oracle."""
-    mp.spawn(_worker, args=(world, _free_port(), implicit, chunks, str(tmp_path), pipeline),
-             nprocs=world, join=True)
+@pytest.mark.parametrize("implicit,chunks,world,pipeline,exchange",
+                         [(False, None, 2, None, "ring"), (True, None, 2, None, "ring"),
+                          (False, 3, 2, True, "ring"), (True, 3, 2, True, "ring"),
+                          (False, 3, 2, None, "ring"), (True, 3, 2, "auto", "ring"),
+                          (False, 2, 8, True, "ring"), (True, 2, 8, True, "ring"),
+                          (True, None, 8, None, "ring"),
+                          (False, 3, 2, True, "peers"), (True, 2, 8, True, "peers"),
+                          (False, None, 8, None, "peers")])
+def test_sharded_als_matches_single_process(tmp_path, implicit, chunks, world, pipeline,
+                                            exchange):
+    """chunks=3: the [C, world, rows] layout with async per-chunk exchanges; with several
+    ranks and >= 2 chunks, pipeline=True pipelines the item half-sweep: the item rows'
+    early partials (users of chunks 0..C-2, every later source row poisoned with NaN in
+    the oracle kernels) are formed while the last user chunk's exchange is in flight,
+    the late ones after (all item chunks on one shared workspace, one Y prep per part);
+    None (the default) runs the plain chunked exchange, "auto" asks the exchange model
+    at the fit's rank (never for these tiny shapes).  exchange="peers": batched isend /
+    irecv to every peer instead of the ring all-gather.  world 8: the target world size
+    of BASELINE configs[3] (8 x MI355X), every rank a range of ~15 users and ~11 items,
+    the full 3-iteration fit against the single-process oracle."""
+    mp.spawn(_worker, args=(world, _free_port(), implicit, chunks, str(tmp_path), pipeline,
+                            exchange), nprocs=world, join=True)
     d = np.load(tmp_path / f"dist_{int(implicit)}_{chunks}_{world}.npz")
-    # (the exchange model never pipelines these tiny shapes by itself)
-    assert bool(d["pipeline"]) == bool(pipeline)
+    assert bool(d["pipeline"]) == (pipeline is True)
     from oracle import als_oracle as O
     u, i, r = planted(120, 90, density=0.08, seed=21, heavy_items=(3,), dup=10)
     if implicit:
@@ -610,16 +617,35 @@ def test_collective_size_guard_refuses_oversized_calls(tmp_path):
 
 
 def test_pipeline_choice_follows_the_exchange_model():
-    """The item half-sweep is pipelined by default only where the hidden all-gather
-    outweighs the partial-slot traffic: the weak-scaled configs[1] shape
-    on 8 ranks (2 chunks, 8 x 162,541 users, 59,047 items: ~7.4k item rows of ~3.4k
-    ratings per rank) — yes; configs[3] on 8 ranks (6 chunks, 10M users, 125k items
-    of ~1k ratings per rank, rank-128 slots) — no; one rank or one chunk — never."""
+    """pipeline="auto" pipelines the item half-sweep only where the hidden all-gather
+    outweighs the partial-slot traffic plus the extra Y prep, at the
+    fit's rank and task length: the weak-scaled configs[1] shape on 8 ranks (2 chunks,
+    8 x 162,541 users, 59,047 items: ~7.4k item rows of ~3.4k ratings per rank, rank
+    64) — yes; configs[3] on 8 ranks (6 chunks, 10M users, 125k items of ~8k ratings
+    per rank, rank-128 slots, 16384-rating tasks) — no; one rank or one chunk — never."""
     from als_mi355x.distributed import ShardedALS, PAD_CAP
     import math
     rpc1 = math.ceil(PAD_CAP * 8 * 162541 / (8 * 2))
     assert ShardedALS.pipeline_pays(8, 2, rpc1, 59047 // 8, 8 * 25_000_095 // 8, rank=64)
+    c1 = ShardedALS.pipeline_cost(8, 2, rpc1, 59047 // 8, 8 * 25_000_095 // 8, rank=64)
+    assert 0 < c1["added_s"] < 0.5 * c1["hidden_s"]
+    # the prep over the arrived prefix of U is part of what the pipeline adds
+    c1b = ShardedALS.pipeline_cost(8, 4, rpc1 // 2, 59047 // 8, 8 * 25_000_095 // 8, rank=64)
+    assert c1b["added_s"] > c1["added_s"]
     rpc3 = math.ceil(PAD_CAP * 10_000_000 / (8 * 6))
-    assert not ShardedALS.pipeline_pays(8, 6, rpc3, 1_000_000 // 8, 10 ** 9 // 8, rank=128)
+    assert not ShardedALS.pipeline_pays(8, 6, rpc3, 1_000_000 // 8, 10 ** 9 // 8, rank=128,
+                                        chunk=16384)
+    # the model follows the rank: a rank-16 fit's slots are far smaller
+    assert ShardedALS.pipeline_cost(8, 6, rpc3, 1_000_000 // 8, 10 ** 9 // 8, rank=16)[
+        "added_s"] < ShardedALS.pipeline_cost(8, 6, rpc3, 1_000_000 // 8, 10 ** 9 // 8,
+                                              rank=128)["added_s"]
     assert not ShardedALS.pipeline_pays(1, 4, rpc1, 59047, 25_000_095)
     assert not ShardedALS.pipeline_pays(8, 1, rpc1, 59047 // 8, 25_000_095)
+
+
+def test_constructor_argument_checks():
+    from als_mi355x.distributed import ShardedALS
+    with pytest.raises(ValueError, match="exchange"):
+        ShardedALS.__init__(object.__new__(ShardedALS), [0], [0], [1.0], exchange="tree")
+    with pytest.raises(ValueError, match="pipeline"):
+        ShardedALS.__init__(object.__new__(ShardedALS), [0], [0], [1.0], pipeline="yes")

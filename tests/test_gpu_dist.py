@@ -46,8 +46,8 @@ def test_sharded_one_rank_matches_engine(implicit, chunks, pipeline, rank):
         core.fit(rank, 3, 0.1, implicit=implicit, alpha=3.0, U0=U0)
         # chunks=3: the chunked [C, world, rows] layout with async per-chunk all-gathers
         sh = ShardedALS(u, i, r, device="cuda:0", chunks=chunks, pipeline=pipeline)
-        assert sh.pipeline == bool(pipeline)
         sh.fit(rank, 3, 0.1, implicit=implicit, alpha=3.0, U0_global=U0)
+        assert sh.pipeline == bool(pipeline)
         _, Us = sh.user_factors()
         _, Vs = sh.item_factors()
         eu = rel_row_err(Us.cpu().numpy(), core.U[:, :rank].cpu().numpy())

@@ -69,9 +69,9 @@ def test_configs3_sharded_one_rank_matches_engine(monkeypatch):
         monkeypatch.setattr(Dm.dist, name, counted(name))
     try:
         u, i, r = D.big_config("big1b", device=DEV)
-        # the sharded engine's task length (its blocks are scheduled once, at setup): the
-        # same per-row arithmetic on both sides
-        core = E.ALSCore(u, i, r, device=DEV, chunk=E.DEFAULT_CHUNK)
+        # both engines pick the fit's task length (engine.chunk_for: 16384 ratings for
+        # explicit rank 128): the same per-row arithmetic on both sides
+        core = E.ALSCore(u, i, r, device=DEV)
         sh = Dm.ShardedALS(u, i, r, device=DEV)  # auto chunks, as bench.py configs3
         del u, i, r
         torch.cuda.empty_cache()
@@ -104,6 +104,8 @@ def test_configs3_sharded_one_rank_matches_engine(monkeypatch):
         report("configs3_sharded_vs_engine_one_iteration",
                {"V_max_row_rel": ev, "U_max_row_rel": eu, "chunks": sh.users.chunks,
                 "collectives": calls, "exchange": sh.exchange_stats(RANK)})
+        assert all(b.chunk == E.chunk_for(RANK, False) for b in sh.user_blocks + sh.item_blocks
+                   if b is not None)
         assert ev <= 1e-6 and eu <= 1e-6, (ev, eu)
     finally:
         dist.destroy_process_group()

@@ -249,8 +249,15 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
                       "note": "f16 matrix-core flops issued (split-f16 Gram: 3 MFMAs per "
                               "fp32-grade product) + the solve's tile products"},
         "fp32_grade_view": {"algorithmic_flops_per_launch": tfa / n,
-                            "achieved_tflops": tfa / te / 1e12, "peak_tflops": PEAK_FP32_TFLOPS},
+                            "achieved_tflops": tfa / te / 1e12, "peak_tflops": PEAK_FP32_TFLOPS,
+                            "note": "Spark's fp32-grade algorithmic flops priced against the fp32 "
+                                    "dense MFMA peak, a unit this kernel does not issue (it runs "
+                                    "split-f16 MFMA: see mfma_view); not the roofline"},
     })
+    # where the counter fields come from: separate rocprofv3 --pmc passes of this workload
+    # (not this run), folded into the committed summary
+    out["counters_source"] = ("profiles/pmc_summary.json: rocprofv3 --pmc passes of this "
+                              "workload (tools/gpu_pmc.sh), not measured in this run")
     busy = {k_: x / te for k_, x in busy_w.items()} if busy_w else {}
     if busy:
         out["limiter"] = max(busy, key=busy.get)
@@ -265,26 +272,34 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
     # bound (contract: hbm | mfma) follows the counter limiter of the launches: "hbm"
     # when the DRAM side is the busiest, "mfma" when the issue side is (VALU busy includes
     # the 8 of every 16 cycles an f16 MFMA holds the vector issue port, so a VALU limiter
-    # is the compute side too).  Compute-bound: achieved = Spark's algorithmic flops
-    # (symmetric Gram + rhs + Cholesky + solves, fp32-grade) / event time against the
-    # dense fp32 MFMA peak — the dtype's; the f16 issue view (mfma_view) and the
-    # algorithmic-bytes view (hbm_view) stay beside it.
+    # is the compute side too).  Compute-bound: achieved = the f16 matrix-core flops the
+    # kernel issues (PMC-counted where profiled, else modelled) / event time against the
+    # dense f16 MFMA peak — the unit the kernel runs in; the fp32-grade view (Spark's
+    # algorithmic flops vs the fp32 peak) and the algorithmic-bytes view (hbm_view) stay
+    # beside it.
     if busy:
         bound = "hbm" if out["limiter"] == "hbm" else "mfma"
     else:
         bound = "hbm" if out["hbm_view"]["frac"] >= out["fp32_grade_view"]["achieved_tflops"] / \
             PEAK_FP32_TFLOPS else "mfma"
-    out["fp32_grade_view"]["frac"] = out["fp32_grade_view"]["achieved_tflops"] / PEAK_FP32_TFLOPS
+    out["fp32_grade_view"]["frac_of_fp32_peak"] = \
+        out["fp32_grade_view"]["achieved_tflops"] / PEAK_FP32_TFLOPS
+    pmc_f = [L.get("mfma_issued_flops_pmc") for L in out["launches"].values()]
+    if all(x for x in pmc_f):
+        out["mfma_view"]["issued_flops_per_launch_pmc"] = sum(pmc_f) / n
+        out["mfma_view"]["achieved_tflops_pmc"] = sum(pmc_f) / te / 1e12
     if bound == "hbm":
         achieved, peak, unit, frac = hbm, PEAK_HBM_GBS, "GB/s", out["hbm_view"]["frac"]
     else:
-        achieved, peak, unit = tfa / te / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"
+        achieved = out["mfma_view"].get("achieved_tflops_pmc", mf)
+        peak, unit = PEAK_F16_MFMA_TFLOPS, "TFLOP/s"
         frac = achieved / peak
     out.update({"bound": bound, "achieved": achieved, "peak": peak, "unit": unit, "frac": frac,
                 "traffic": traffic / n if (have_traffic and traffic > 0) else None})
     if have_trace and tr > 0:
+        issued = sum(pmc_f) if all(x for x in pmc_f) else tf
         out["frac_pmc_profile"] = (tb / tr / 1e9 / PEAK_HBM_GBS) if bound == "hbm" else \
-            (tfa / tr / 1e12 / PEAK_FP32_TFLOPS)
+            (issued / tr / 1e12 / PEAK_F16_MFMA_TFLOPS)
         out["pmc_profile_avg_launch_us"] = 1e6 * tr / n
     return out
 

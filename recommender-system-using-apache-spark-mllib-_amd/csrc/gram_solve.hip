@@ -60,6 +60,13 @@ constexpr int kRescueGrid = 64;
 // the diagonal stays within a few times lambda n); implicit confidences spanning six
 // decades spread by 1e3-1e5 and reach 1e-3 errors in fp32.
 constexpr float kCondMax = 32.f;
+// The same limit for the implicit rows of the rank 65-128 (W1) solve, which has no
+// iterative refinement (ranks <= 64 refine every implicit row against Spark's fp64
+// residual): implicit counts 1..1e6 at rank 128 left rows with spreads in (8, 32] at
+// 4.9e-6..5.6e-6 against the fp64 oracle; at 8 every row of that test is within 8.4e-8
+// (the rows beyond it re-solved in fp64) and configs[2] re-solves none (its item rows
+// spread 2-4, user rows < 2): 9.01 / 9.09 ms/iter at 32 / 8, profiles/r06/ab_cond_implicit.txt.
+constexpr float kCondMaxImplicit = 8.f;
 constexpr int kMaxRank = 128;
 
 template <int CN>
@@ -1638,7 +1645,8 @@ __device__ __forceinline__ half8v dup_lo(const half8v& v) {
 // = solution entry of variable (block c, index m), every row group q.
 template <int NB, bool SPLIT = kW1SplitSchur<NB>>
 __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
-                                           float* __restrict__ lds, int k, float (&xcol)[NB]) {
+                                           float* __restrict__ lds, int k, float (&xcol)[NB],
+                                           float cond_max = kCondMax) {
   using L = W1LdsT<NB>;
   constexpr int CS = L::CS;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
@@ -1839,7 +1847,7 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
   rmax = fmaxf(rmax, dpp_f<0x141>(rmax));
   rmin = fminf(rmin, dpp_f<0x140>(rmin));
   rmax = fmaxf(rmax, dpp_f<0x140>(rmax));
-  return dmin > 0.f && rmin > 0.f && rmax <= kCondMax * rmin && __ballot(!fin) == 0;
+  return dmin > 0.f && rmin > 0.f && rmax <= cond_max * rmin && __ballot(!fin) == 0;
 }
 
 // w1_solve_x, then the solution row written un-permuted: dim d = i * NB + c <->
@@ -1847,9 +1855,10 @@ __device__ __forceinline__ bool w1_solve_x(floatx4 (&A)[NB * (NB + 1) / 2], floa
 template <int NB, bool SPLIT = kW1SplitSchur<NB>>
 __device__ __forceinline__ bool w1_solve(floatx4 (&A)[NB * (NB + 1) / 2], float (&bcol)[NB],
                                          float* __restrict__ lds, int k,
-                                         float* __restrict__ xrow, int ld) {
+                                         float* __restrict__ xrow, int ld,
+                                         float cond_max = kCondMax) {
   float xcol[NB];
-  const bool ok = w1_solve_x<NB, SPLIT>(A, bcol, lds, k, xcol);
+  const bool ok = w1_solve_x<NB, SPLIT>(A, bcol, lds, k, xcol, cond_max);
   const int lane = threadIdx.x & 63, m = lane & 15;
   if (lane < 16) {
 #pragma unroll
@@ -2150,7 +2159,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
-                                                    RescueList rl);
+                                                    RescueList rl, float cond_max = kCondMax);
 
 // (k <= 64 keeps one gather step in flight: two steps need 187 registers, i.e. two
 // waves per SIMD instead of three, measured slower on configs[1]: 2.07 -> 2.24 ms/iter.)
@@ -2437,7 +2446,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
                                                     const float* __restrict__ ytyC,
                                                     unsigned char* smem, int k, float reg,
                                                     float* __restrict__ xrow, int ld, int row,
-                                                    RescueList rl) {
+                                                    RescueList rl, float cond_max) {
   constexpr int NT_ = NB * (NB + 1) / 2;
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
   const float inv = 1.f / scale;  // power of two: exact
@@ -2477,7 +2486,7 @@ __device__ __forceinline__ void w1_finish_and_solve(floatx4 (&A)[NB * (NB + 1) /
       }
     });
   }
-  const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld);
+  const bool ok = w1_solve<NB, SPLIT>(A, bq, reinterpret_cast<float*>(smem), k, xrow, ld, cond_max);
   if (!ok) rescue_append(rl, row);  // re-solved in fp64
 }
 
@@ -2558,7 +2567,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
   w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
-                                               X + (int64_t)row * ld, ld, row, rl);
+                                               X + (int64_t)row * ld, ld, row, rl,
+                                               IMPLICIT ? kCondMaxImplicit : kCondMax);
 }
 
 // ---------------------------------------------------------------------------
@@ -2863,7 +2873,7 @@ __global__ __launch_bounds__(64, 1) void reduce_solve_w1_kernel(
     }
   }
   w1_finish_and_solve<false>(A, 1.f, bt, n_reg, nullptr, smem, k, reg, X + (int64_t)row * ld, ld,
-                             row, rl);
+                             row, rl, IMPLICIT ? kCondMaxImplicit : kCondMax);
 }
 
 // Rescue launch: every row the fp32-grade path did not solve to the 1e-4 bar — its

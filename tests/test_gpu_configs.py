@@ -99,9 +99,15 @@ def test_configs1_csr_full_size_bitexact(ml25m):
         np.testing.assert_array_equal(block.val.cpu().numpy(), val_)
 
 
-def _half_sweeps(core, rank, implicit, alpha, tag):
+def _half_sweeps(core, rank, implicit, alpha, tag, warm=0):
+    """One item and one user half-sweep against the C oracle from identical source
+    factors: the seeded start (warm = 0) or the factors after `warm` production
+    iterations (a converged state: the factors carry the data's low-rank structure and
+    the systems are less well conditioned than at the random start)."""
     reg = 0.1
     core.init_factors(rank, seed=5)
+    for _ in range(warm):
+        core.iterate(reg, implicit, alpha)
     U0 = core.U[:, :rank].cpu().numpy()
     core.status.zero_()
     core.half_sweep_items(reg, implicit, alpha)
@@ -133,6 +139,16 @@ def _half_sweeps(core, rank, implicit, alpha, tag):
 def test_configs1_half_sweeps_rank64(ml25m):
     core, _ = ml25m
     _half_sweeps(core, 64, False, 1.0, "configs1_rank64")
+
+
+def test_configs1_half_sweeps_rank64_after_10_iterations(ml25m):
+    core, _ = ml25m
+    _half_sweeps(core, 64, False, 1.0, "configs1_rank64_after10", warm=10)
+
+
+def test_configs2_half_sweeps_rank128_implicit_after_10_iterations(ml25m):
+    core, _ = ml25m
+    _half_sweeps(core, 128, True, 40.0, "configs2_rank128_implicit_after10", warm=10)
 
 
 def test_configs2_half_sweeps_rank128_implicit(ml25m):

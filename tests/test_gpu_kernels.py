@@ -603,8 +603,10 @@ def test_implicit_counts_spanning_six_decades(rank, seed):
     and fp32 LDL^T alone turn into 1e-4..4e-3 errors (emulated).  At rank <= 64 every
     implicit row is iteratively refined against Spark's fp64 residual (rows that do not
     converge go to the fp64 rescue); at rank 65-128 the W1 solve's pivot-spread test
-    routes ill-conditioned rows to the rescue.  Every row (light rows and the chunked
-    heavy item) must match the oracle to 1e-5 — a 10x margin under the 1e-4 bar."""
+    routes rows whose pivots spread beyond 8 (kCondMaxImplicit) to the fp64 rescue.
+    Every row (light rows and the chunked heavy item) must match the oracle to 2e-6 at
+    ranks <= 64 (measured <= 7.1e-7) and 1e-6 at rank 128 (measured <= 8.4e-8; 5.6e-6
+    with round 5's limit of 32) — 50-100x under the 1e-4 bar."""
     u, i, _ = planted(500, 300, density=0.06, heavy_items=(4,), seed=43 + 10 * seed)
     rng = np.random.default_rng(6 + seed)
     r = np.round(10.0 ** rng.uniform(0, 6, u.size)).astype(np.float32)
@@ -619,7 +621,7 @@ def test_implicit_counts_spanning_six_decades(rank, seed):
                          U0, 0.1, True, 1.0)
     e = _exact_rel_errs(core.V[:, :rank].cpu().numpy(), V_ref)
     report(f"implicit_counts_1_1e6[rank={rank},seed={seed}]", float(e.max()))
-    assert e.max() <= 1e-5, float(e.max())
+    assert e.max() <= (1e-6 if rank > 64 else 2e-6), float(e.max())
 
 
 def test_failed_pivot_raises_with_row():

@@ -102,7 +102,17 @@ def main():
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
     core.check_status()
-    out = {"wl": wl, "lib": _lib_loaded(), "chunk": chunk,
+    rescued = {}
+    for name, block, Y, X, n_src in (("item", core.item_block, core.U, core.V, core.n_users),
+                                     ("user", core.user_block, core.V, core.U, core.n_items)):
+        yty = E.compute_yty(Y, n_src, k, core.ws) if imp else None
+        E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
+                     E.PHASE_ALL & ~E.PHASE_RESCUE)
+        torch.cuda.synchronize()
+        rescued[name] = int(core.ws.buf[8:12].view(torch.int32).item())  # rescue count word
+        E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws, E.PHASE_RESCUE)
+    torch.cuda.synchronize()
+    out = {"wl": wl, "lib": _lib_loaded(), "chunk": chunk, "rescued": rescued,
            "dual_max": E.DUAL_MAX_RATINGS,
            "ms_per_iter": round(ms, 4)}
     if "--no-parity" not in sys.argv:

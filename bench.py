@@ -73,6 +73,9 @@ PEAK_FP32_TFLOPS = 157.3
 PEAK_F16_MFMA_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_summary.json")
+# measured random-row gather rate from an Infinity-Cache-resident table (38 MB, 1,152-B
+# rows into LDS; /opt/skills/guides/MI355X_MICROARCH.md "Indexed rows: gather into LDS")
+GATHER_IC_GBS = 8600.0
 TOPK_WARM_ROWS = 65536
 
 
@@ -244,6 +247,14 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
         "avg_launch_us": 1e6 * te / n,
         "algorithmic_bytes_per_launch": tb / n,
         "hbm_view": {"achieved_gbs": hbm, "peak_gbs": PEAK_HBM_GBS, "frac": hbm / PEAK_HBM_GBS},
+        # the factor tables of a half-sweep (ML-25M shape: 15-42 MB split tables) sit in
+        # the 256 MB Infinity Cache, so the rate the per-rating row gathers can reach is
+        # the guide's measured random-row gather rate from such a table, not HBM's
+        "gather_view": {"achieved_gbs": hbm, "peak_gbs": GATHER_IC_GBS,
+                        "frac": hbm / GATHER_IC_GBS,
+                        "note": "vs 8.6 TB/s: random 1,152-B rows gathered into LDS from a 38 MB "
+                                "table (Infinity Cache), MI355X_MICROARCH.md 'Indexed rows'; this "
+                                "kernel gathers 256-B (k=64) / 512-B (k=128) rows"},
         "mfma_view": {"issued_flops_per_launch": tf / n, "achieved_tflops": mf,
                       "peak_tflops": PEAK_F16_MFMA_TFLOPS, "frac": mf / PEAK_F16_MFMA_TFLOPS,
                       "note": "f16 matrix-core flops issued (split-f16 Gram: 3 MFMAs per "

@@ -204,11 +204,14 @@ int als_rmse_partial(const int32_t* u, const int32_t* i, const float* r, int64_t
  * top: V is swept with hi.hi alone against the row's k-th score minus a proven
  * bound on the dropped terms, and blocks past it get the full hi.hi + hi.lo + lo.hi
  * score, so every listed pair carries its exact split score.  Lists: registers of
- * one owner lane for top <= 16, four-lane ("quad") register lists for top <= 128,
- * sorted LDS lists above.  Rows of V holding NaN score NaN and are never listed.
+ * one owner lane for top <= 16; for top <= 128 the running top scores in four-lane
+ * ("quad") register lists and every key reaching the row's k-th score in a per-row
+ * log in the workspace, from which the exact top keys are selected; sorted LDS lists
+ * above.  Rows of V holding NaN score NaN and are never listed.
  * k <= 128, top <= 256.  The n_q x n_v score matrix is never materialised.
  * Workspace (16-byte aligned): scale words, the hi and lo f16 planes of V in sweep
- * (decreasing norm) order, the order, bucket counts and the scaled row norms. */
+ * (decreasing norm) order, the order, bucket counts, the scaled row norms and, for
+ * 16 < top <= 128, the key logs (1,024 keys per query row of up to 4,096 x 128 rows). */
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top);
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v,
              int32_t ld, int32_t k, int32_t top,

@@ -388,13 +388,23 @@ typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef _Float16 half8v __attribute__((ext_vector_type(8)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 
-// Round-to-nearest packed conversions (v_cvt_pk_f16_f32): unbiased pieces; the
-// residual t - hi is exact in fp32.
-__device__ __forceinline__ void split_pair(float t0, float t1, uint32_t& hi, uint32_t& lo) {
-  const half2v h = __builtin_convertvector((float2v){t0, t1}, half2v);
-  const half2v l = __builtin_convertvector((float2v){t0 - (float)h[0], t1 - (float)h[1]}, half2v);
-  hi = __builtin_bit_cast(uint32_t, h);
-  lo = __builtin_bit_cast(uint32_t, l);
+// The split of two weighted values w0 y0, w1 y1 straight from the fp32 operands:
+// hi = f16(w y) and lo = f16(w y - hi), each one v_fma_mix (the product and the
+// residual formed inside one fp32 fma; lo also keeps the product's own fp32 rounding
+// error), 4 VALU per pair instead of a multiply, a packed convert, two converts back,
+// a subtract and a packed convert (round 5): configs[2] 9.11 -> 9.06 ms/iter,
+// profiles/r06/ab_fma_mix_split.jsonl.
+__device__ __forceinline__ void split_pair_w(float y0, float w0, float y1, float w1, uint32_t& hi,
+                                             uint32_t& lo) {
+  uint32_t h, l;
+  asm("v_fma_mixlo_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "=v"(h) : "v"(y0), "v"(w0));
+  asm("v_fma_mixhi_f16 %0, %1, %2, 0 op_sel_hi:[0,0,0]" : "+v"(h) : "v"(y1), "v"(w1));
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel:[0,0,0] op_sel_hi:[0,0,1]"
+      : "=v"(l) : "v"(y0), "v"(w0), "v"(h));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "+v"(l) : "v"(y1), "v"(w1), "v"(h));
+  hi = h;
+  lo = l;
 }
 
 __device__ __forceinline__ half8v as_h8(const uint32_t (&v)[4]) {
@@ -484,7 +494,7 @@ __device__ __forceinline__ void split_prepare(const SplitStep<TS::NC>& s,
   for (int c = 0; c < TS::NC; ++c)
 #pragma unroll
     for (int p = 0; p < 4; ++p)
-      split_pair(w[2 * p] * s.y[2 * p][c], w[2 * p + 1] * s.y[2 * p + 1][c], hi[c][p], lo[c][p]);
+      split_pair_w(s.y[2 * p][c], w[2 * p], s.y[2 * p + 1][c], w[2 * p + 1], hi[c][p], lo[c][p]);
 }
 
 // Part 2 (matrix cores): 3 f16 MFMAs per tile.

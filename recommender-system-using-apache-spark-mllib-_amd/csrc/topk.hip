@@ -425,13 +425,14 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // LDS (one ds_write_b128 per lane); each owner lane takes its row's survivors
 // from the ballots, inserts them, and the new k-th scores go back to the
 // filtering lanes through LDS.  16 < top <= 128 (TOPR = 32 / 64 / 100 / 128, one
-// row group): quad lists — a row's list is split over its four lanes 16j + rho as
-// sorted sub-lists of TOPR / 4 keys; the row's k-th best is the least of their
-// four minima (two lane swaps), an insertion replaces that minimum in the lane
-// holding it, and every row of the wave inserts in the same pass (the LDS path
+// row group): quad lists — a row's running top scores are split over its four lanes
+// 16j + rho as sorted sub-lists of TOPR / 4 scores; the row's k-th best is the least
+// of their four minima (two lane swaps), a better score replaces that minimum in the
+// lane holding it, and every row of the wave inserts in the same pass (the LDS path
 // below inserts one candidate per wave at a time: 70 ms vs 13.6 ms of scores at
-// rank 128 top 100 on the ML-25M shape).  The output ranks each entry by counting
-// the larger keys of the four sub-lists.
+// rank 128 top 100 on the ML-25M shape).  Every key reaching the k-th score (ties
+// included) is appended to the row's log in global memory; the output is the exact
+// top `top` keys of the log (tk_log_kth), ranked.
 // TOPR = 0 (top > 128): sorted lists in LDS, wave-cooperative insertion
 // (topk_offer), 4 wavefronts.
 // Tile rows (hi halves only, RW = 4 NK uint4 per row): register lists (8
@@ -478,12 +479,14 @@ __device__ __forceinline__ void tk_insert(uint64_t (&kv)[TOPR], uint64_t c) {
 
 // Quad lists (16 < top <= 128, one row group per workgroup): row rho of a wave is
 // owned by its four lanes 16j + rho, each holding a sorted sub-list of S = TOPR / 4
-// keys (sub-list j has top / 4 (+1 for j < top % 4) live slots, sentinels above).
-// The union is the row's current top set; its k-th best is the smallest [0] of the
-// four, found by two row swaps.  An insertion replaces that minimum in the lane that
-// holds it (tk_insert drops [0]), so the sub-list sizes never change; the rows of a
-// wave insert in parallel, one candidate per row per pass.
-__device__ __forceinline__ uint64_t tk_min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+// SCORES (sub-list j has top / 4 (+1 for j < top % 4) live slots, +inf sentinels
+// above, -inf while open).  The union is the row's running top scores; its k-th best
+// is the smallest [0] of the four, found by two row swaps.  A better score replaces
+// that minimum in the lane that holds it (tk_insert_f drops [0]), so the sub-list
+// sizes never change; the rows of a wave insert in parallel, one candidate per row per
+// pass.  The (score, index) keys themselves go to the row's log (below); round 5 kept
+// the 64-bit keys in the sub-lists (224 registers, configs[4] sample top-100 191 ms,
+// vs 198 registers and 177 ms now: profiles/r06/ab_topk_logs.txt).
 
 // Value of x in lane (j ^ 1, rho) (X = 16) or (j ^ 2, rho) (X = 32), j = lane / 16.
 template <int X>
@@ -497,14 +500,56 @@ __device__ __forceinline__ uint32_t tk_partner(uint32_t x) {
   const int j = (threadIdx.x & 63) >> 4;
   return (j & (X / 16)) ? a : b;
 }
-template <int X>
-__device__ __forceinline__ uint64_t tk_partner64(uint64_t x) {
-  return ((uint64_t)tk_partner<X>((uint32_t)(x >> 32)) << 32) | tk_partner<X>((uint32_t)x);
+// Smallest score over the four lanes of this lane's row.
+__device__ __forceinline__ float tk_quad_minf(float x) {
+  x = fminf(x, __uint_as_float(tk_partner<16>(__float_as_uint(x))));
+  return fminf(x, __uint_as_float(tk_partner<32>(__float_as_uint(x))));
 }
-// Smallest key over the four lanes of this lane's row.
-__device__ __forceinline__ uint64_t tk_quad_min(uint64_t x) {
-  x = tk_min_u64(x, tk_partner64<16>(x));
-  return tk_min_u64(x, tk_partner64<32>(x));
+
+// Insert score c into a sorted ascending score sub-list (its least at [0], +inf
+// sentinels past the live slots), dropping [0]; the caller has checked c > [0].
+template <int N>
+__device__ __forceinline__ void tk_insert_f(float (&sv)[N], float c) {
+  bool gt[N + 1];
+#pragma unroll
+  for (int j = 0; j < N; ++j) gt[j] = c > sv[j];
+  gt[N] = false;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float nx = j + 1 < N ? sv[j + 1] : 0.f;
+    sv[j] = gt[j + 1] ? nx : (gt[j] ? c : sv[j]);
+  }
+}
+
+// Per-row key logs (16 < top <= 128).  Every (score, index) key that reaches its row's
+// running top is appended to the row's log in global memory (kTkLogCap keys per row);
+// the registers keep only the scores (the quad sub-lists above), which is all the
+// filter needs.  At the end of the sweep the row's `top` largest keys are selected from
+// its log exactly (tk_log_select), and a log about to overflow is compacted to them.
+constexpr int kTkLogCap = 1024;
+constexpr int kTkLogJ = kTkLogCap / 64;  // keys per lane when a wave holds a whole log
+// Query-row blocks per launch with logs (one log slab per block of a launch: at most
+// 512 x 128 rows x 8 KB = 512 MB; a larger n_q runs in launches of this many blocks).
+// All 10M users of configs[4], top-100: 6,733 ms with 512-block launches, 6,750 ms
+// with 4096 (profiles/r06/ab_topk_logs.txt).  (A grid-stride loop over the blocks
+// inside the kernel instead took every top-k kernel's registers to the 256 limit and
+// spilled: not used.)
+constexpr int kTkLogBlocks = 512;
+
+// The T-th largest of the n keys of log L (n <= kTkLogCap, 1 <= T <= n), by a bitwise
+// search over the 64 key bits: the largest P with #{keys >= P} >= T.  Keys are unique
+// ((score, V row) pairs), so exactly T keys are >= P.  The wave's lanes hold the keys
+// (kv[j] = L[64 j + lane], 0 past n: below every real key).
+__device__ __forceinline__ uint64_t tk_log_kth(const uint64_t (&kv)[kTkLogJ], int T) {
+  uint64_t P = 0;
+  for (int b = 63; b >= 0; --b) {
+    const uint64_t cand = P | (1ull << b);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < kTkLogJ; ++j) c += __popcll(__ballot(kv[j] >= cand));
+    if (c >= T) P = cand;
+  }
+  return P;
 }
 
 // Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
@@ -521,7 +566,8 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
                                                          int64_t n_v, int ld, int k, int top,
                                                          const float* __restrict__ scal,
                                                          int32_t* __restrict__ idx_out,
-                                                         float* __restrict__ score_out) {
+                                                         float* __restrict__ score_out,
+                                                         uint64_t* __restrict__ tlog) {
   constexpr int NW = tk_nw(TOPR);  // wavefronts
   constexpr int GR = 16 * NW;          // query rows of a row group
   constexpr int KQ = 32 * NK;
@@ -606,19 +652,54 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   if (TOPR > 0 && lane < 16 * RG)
     thr[lane] = ((live[lane >> 4] >> (lane & 15)) & 1u) ? -__builtin_inff() : __builtin_inff();
   bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
-  // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its
-  // sub-list of row m (every lane: sub-list q)
+  // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its score
+  // sub-list of row m (every lane: sub-list q of each row group) with the row's keys
+  // in its log (tlog)
   constexpr bool QUAD = TOPR > 16;
-  static_assert(!QUAD || (RG == 1 && TOPR % 4 == 0), "quad lists: one row group");
+  static_assert(!QUAD || TOPR % 4 == 0, "quad lists: TOPR / 4 per lane");
   // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
   constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
   constexpr int KG = QUAD ? RG : 1;  // quad: one sub-list per row group in every lane
   const int ncap = QUAD ? top / 4 + (q < top % 4 ? 1 : 0) : top;  // live slots of this list
-  uint64_t kv[KG][NR];
+  uint64_t kv[QUAD ? 1 : KG][QUAD ? 1 : NR];
+  float sv[QUAD ? KG : 1][QUAD ? NR : 1];
+  int lcnt[QUAD ? KG : 1];  // QUAD: keys in row m's log (the same in its four lanes)
+  if constexpr (QUAD) {
 #pragma unroll
-  for (int g = 0; g < KG; ++g)
+    for (int g = 0; g < KG; ++g) {
+      lcnt[g] = 0;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) kv[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
+      for (int j = 0; j < NR; ++j) sv[g][j] = j < ncap ? -__builtin_inff() : __builtin_inff();
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int j = 0; j < NR; ++j) kv[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
+  }
+  // QUAD: row (group g, row rho of this wave)'s log: kTkLogCap keys in this block's slab
+  auto rowlog = [&](int g, int rho) -> uint64_t* {
+    return tlog + ((int64_t)blockIdx.x * GR * RG + GR * g + 16 * w + rho) * kTkLogCap;
+  };
+  // QUAD: keep the `top` largest keys of row (g, rho)'s log (n > top keys), in place
+  auto log_compact = [&](int g, int rho, int n) {
+    uint64_t* L = rowlog(g, rho);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's appends have landed
+    uint64_t kl[kTkLogJ];
+#pragma unroll
+    for (int j = 0; j < kTkLogJ; ++j) kl[j] = 64 * j + lane < n ? L[64 * j + lane] : 0ull;
+    const uint64_t P = tk_log_kth(kl, top);
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < kTkLogJ; ++j) {
+      const bool kp = kl[j] >= P;
+      const uint64_t b = __ballot(kp);
+      const int pos = base + __popcll(b & ((1ull << lane) - 1));
+      if (kp) L[pos] = kl[j];
+      base += __popcll(b);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
 
   // Tile staging by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write): the
   // workgroup's waves each issue NI / NW of the tile's 1 KB pieces.  Tile row r, uint4 c
@@ -761,19 +842,24 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
           const int mm = act ? __builtin_ctz(msk[g]) : 0;
           msk[g] &= msk[g] - 1;
           const float sc = st[g * 256 + rho + 16 * mm];
-          const uint64_t c = (act && sc == sc) ? tk_key(sc, bperm[mm]) : kTkKeyOpen;
-          const uint64_t gmin = tk_quad_min(kv[g][0]);
-          // the lowest sub-list whose [0] is the row minimum takes the candidate
-          const uint64_t holders = (__ballot(kv[g][0] == gmin) >> rho) & 0x0001000100010001ull;
-          if (c > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert<NR>(kv[g], c);
+          const float gmin = tk_quad_minf(sv[g][0]);
+          // the lowest sub-list whose [0] is the row minimum takes a better score
+          const uint64_t holders = (__ballot(sv[g][0] == gmin) >> rho) & 0x0001000100010001ull;
+          // the four lanes of row rho agree: a score reaching the row's running
+          // k-th (ties included: the index decides at the end) goes to the log
+          if (act && sc == sc && sc >= gmin) {
+            if (q == 0) rowlog(g, rho)[lcnt[g]] = tk_key(sc, bperm[mm]);
+            lcnt[g] += 1;
+            if (sc > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert_f<NR>(sv[g], sc);
+          }
         };
 #pragma unroll
         for (int g = 0; g < KG; ++g)
           while (__ballot(msk[g] != 0)) pass(g);
 #pragma unroll
         for (int g = 0; g < KG; ++g) {
-          const uint64_t gmin = tk_quad_min(kv[g][0]);
-          if (q == 0) thr[16 * g + rho] = gmin == kTkKeyOpen ? -__builtin_inff() : tk_key_score(gmin);
+          const float gmin = tk_quad_minf(sv[g][0]);
+          if (q == 0) thr[16 * g + rho] = gmin;  // -inf while the row has open slots
         }
       } else if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
         const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
@@ -798,7 +884,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
         if constexpr (QUAD) {
 #pragma unroll
           for (int g = 0; g < KG; ++g)
-            open_list = open_list || (((live[g] >> m) & 1u) && kv[g][0] == kTkKeyOpen);
+            open_list = open_list || (((live[g] >> m) & 1u) && lcnt[g] < top);
         } else {
           open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
                       kv[0][0] == kTkKeyOpen;
@@ -852,6 +938,20 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   // buffer buf; false: sweep over
   auto tile_step = [&](int64_t vb) -> bool {
       const uint4* tb = tiles + buf * VT * RW;
+      if constexpr (QUAD) {
+        // a log that this tile could overflow (at most VT appends per row) is cut to
+        // its row's `top` best keys first
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          uint64_t nb = __ballot(q == 0 && lcnt[g] > kTkLogCap - VT) & 0xFFFFull;
+          while (nb) {
+            const int rho = __builtin_ctzll(nb);
+            nb &= nb - 1;
+            log_compact(g, rho, __builtin_amdgcn_readlane(lcnt[g], rho));
+            if (m == rho) lcnt[g] = top;
+          }
+        }
+      }
       nv_cur = n_v > 0 ? vnorm[vb] : 0.f;
       nvt = fmaf(nv_cur, 1.01f, 1.f);
       // early exit: every row of the wave holds a k-th score that no row from this
@@ -879,24 +979,25 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       if (!wdone) {
         floatx4 acc0[RG], acc1[RG];
         if constexpr (TOPR > 0) {
-          static_assert(NC % 4 == 0, "quartets of 16-row blocks per tile");
+          constexpr int NB4 = 4;  // blocks per ballot
+          static_assert(NC % NB4 == 0, "quartets of 16-row blocks per tile");
           // four blocks scored back to back, then one ballot for all four against the
           // current coarse thresholds (they only rise, so a quartet with no pair past
           // them has none past the later ones): the LDS -> MFMA -> compare -> branch
           // latency of a block is paid once per 64 V rows.  Measured on the configs[4]
           // 262,144-user sample against block pairs (the path below): top-10 97.3 ->
           // 91.5 ms, top-100 233 -> 194 ms.
-          floatx4 a4[4][RG];
+          floatx4 a4[NB4][RG];
 #pragma unroll 1
-          for (int c = 0; c < NC; c += 4) {
+          for (int c = 0; c < NC; c += NB4) {
             const uint4* tbr = tb + (16 * c + m) * RW;
             const int* bp = tperm + buf * VP + 16 * c;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
+            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
             if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {
               bool any = false;
 #pragma unroll
-              for (int j = 0; j < 4; ++j)
+              for (int j = 0; j < NB4; ++j)
 #pragma unroll
                 for (int g = 0; g < RG; ++g)
 #pragma unroll
@@ -904,7 +1005,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
               if (__ballot(any) == 0) continue;
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < NB4; ++j)
               filter(a4[j], vb + 16 * (c + j), bp + 16 * j, tbr + 16 * j * RW);
           }
         } else {
@@ -941,67 +1042,51 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   // no LDS-DMA may still be landing when the workgroup ends
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (QUAD) {
-    // output position of a real entry = number of real entries above it in the
-    // row's four sub-lists; open slots (fewer than `top` V rows) fill the tail
-#pragma unroll
+    // each row's `top` largest keys, selected exactly from its log, ranked and written
+    // in order; fewer than `top` keys (n_v < top) leave the tail open
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's log appends landed
+    uint64_t* ks = reinterpret_cast<uint64_t*>(sblk + w * RG * 256);  // <= 128 keys (1 KB)
+#pragma unroll 1
     for (int g = 0; g < KG; ++g) {
-      const uint64_t (&kg)[NR] = kv[g];
-      const int64_t row = qbase + GR * g + 16 * w + m;
-      const bool zero = !((live[g] >> m) & 1u);
-      int rank[NR];
-      int nreal = 0, nopen = 0;
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        nreal += (kg[i] != kTkKeyOpen && kg[i] != kTkKeySentinel) ? 1 : 0;
-        nopen += (i < ncap && kg[i] == kTkKeyOpen) ? 1 : 0;
-      }
-#pragma unroll
-      for (int i = 0; i < NR; ++i) {
-        rank[i] = 0;
-#pragma unroll
-        for (int t = i + 1; t < NR; ++t) rank[i] += kg[t] != kTkKeySentinel ? 1 : 0;
-      }
-      auto count_above = [&](auto pc) {  // entries of sub-list q ^ P above each own entry
-        constexpr int P = decltype(pc)::value;
-#pragma unroll
-        for (int t = 0; t < NR; ++t) {
-          const uint64_t o = P == 1 ? tk_partner64<16>(kg[t])
-                                    : (P == 2 ? tk_partner64<32>(kg[t])
-                                              : tk_partner64<32>(tk_partner64<16>(kg[t])));
-          if (o != kTkKeySentinel) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) rank[i] += o > kg[i] ? 1 : 0;
+#pragma unroll 1
+      for (int rho = 0; rho < 16; ++rho) {
+        const int64_t row = qbase + GR * g + 16 * w + rho;
+        if (row >= n_q) break;
+        if (!((live[g] >> rho) & 1u)) {  // every score 0: the first `top` rows, ties by index
+          for (int e = lane; e < top; e += 64) {
+            idx_out[row * top + e] = e < n_v ? e : -1;
+            score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
           }
+          continue;
         }
-      };
-      count_above(std::integral_constant<int, 1>{});
-      count_above(std::integral_constant<int, 2>{});
-      count_above(std::integral_constant<int, 3>{});
-      const int r1 = (int)tk_partner<16>((uint32_t)nreal), r2 = (int)tk_partner<32>((uint32_t)nreal);
-      const int r3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nreal));
-      const int o1 = (int)tk_partner<16>((uint32_t)nopen), o2 = (int)tk_partner<32>((uint32_t)nopen);
-      const int o3 = (int)tk_partner<32>(tk_partner<16>((uint32_t)nopen));
-      const int R = nreal + r1 + r2 + r3;
-      const int obase = R + ((q ^ 1) < q ? o1 : 0) + ((q ^ 2) < q ? o2 : 0) + ((q ^ 3) < q ? o3 : 0);
-      if (row < n_q) {
-        if (zero) {  // every score 0: the first `top` rows, ties by index
-          if (q == 0) {
-            for (int e = 0; e < top; ++e) {
-              idx_out[row * top + e] = e < n_v ? e : -1;
-              score_out[row * top + e] = e < n_v ? 0.f : -__builtin_inff();
-            }
-          }
-        } else {
+        const int n = __builtin_amdgcn_readlane(lcnt[g], rho);
+        const uint64_t* L = rowlog(g, rho);
+        uint64_t kl[kTkLogJ];
 #pragma unroll
-          for (int i = 0; i < NR; ++i) {
-            if (i < ncap) {
-              const bool real = kg[i] != kTkKeyOpen;
-              const int64_t e = row * top + (real ? rank[i] : obase + i);
-              idx_out[e] = real ? tk_key_index(kg[i]) : -1;
-              score_out[e] = real ? tk_key_score(kg[i]) * unscale : -__builtin_inff();
-            }
-          }
+        for (int j = 0; j < kTkLogJ; ++j) kl[j] = 64 * j + lane < n ? L[64 * j + lane] : 0ull;
+        const int T = n < top ? n : top;
+        const uint64_t P = n > top ? tk_log_kth(kl, T) : 1ull;  // real keys are >= 1
+        int base = 0;
+#pragma unroll
+        for (int j = 0; j < kTkLogJ; ++j) {
+          const bool kp = kl[j] >= P;
+          const uint64_t b = __ballot(kp);
+          if (kp) ks[base + __popcll(b & ((1ull << lane) - 1))] = kl[j];
+          base += __popcll(b);
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int e = lane; e < T; e += 64) {
+          const uint64_t key = ks[e];
+          int r = 0;
+          for (int t = 0; t < T; ++t) r += ks[t] > key ? 1 : 0;
+          idx_out[row * top + r] = tk_key_index(key);
+          score_out[row * top + r] = tk_key_score(key) * unscale;
+        }
+        for (int e = T + lane; e < top; e += 64) {
+          idx_out[row * top + e] = -1;
+          score_out[row * top + e] = -__builtin_inff();
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ks is rewritten for the next row
       }
     }
     return;
@@ -1077,7 +1162,11 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 constexpr int64_t kTkRg2MinRows = 4 * 256 * 256;
 static int topk_split_rg(int k, int top, bool quad, int64_t n_q) {
   const int kq = topk_kq(k);
-  if (quad) return 1;  // quad lists: one row group
+  // quad lists (score sub-lists in registers, keys in per-row logs): one row group.
+  // (Round 6, configs[4] 262,144-user sample, top-100: one group 176.5 ms, two groups
+  // 212.7 ms — two groups' sub-lists and A operands exceed 256 registers, 50 spilled;
+  // round 5's 64-bit key lists: 190 ms.  profiles/r06/ab_topk_logs.txt)
+  if (quad) return 1;
   if (top <= kTopR && n_q < kTkRg2MinRows) return 1;
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
@@ -1095,14 +1184,22 @@ static size_t tk_table_bytes(int64_t n_v, int32_t k) {
   return align_up(4 * (size_t)topk_kq(k) * (size_t)(n_v > 0 ? n_v : 0));
 }
 
+// Per-row key logs of the quad lists (16 < top <= 128): kTkLogCap keys for every query
+// row of one launch's blocks (at most kTkLogBlocks blocks per launch).
+static size_t tk_log_bytes(int64_t n_q, int32_t k, int32_t top) {
+  if (n_q <= 0 || !topk_quad(top, 0)) return 0;
+  const int rg = topk_split_rg(k, top, true, n_q);
+  const int64_t rows = 16 * (int64_t)tk_nw(kTopQ) * rg;  // query rows per block
+  const int64_t blocks = std::min<int64_t>((n_q + rows - 1) / rows, kTkLogBlocks);
+  return align_up(sizeof(uint64_t) * (size_t)(blocks * rows) * kTkLogCap);
+}
+
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top) {
-  (void)n_q;
-  (void)top;
   // 256 B of scale words | split planes of V in sweep order (2 x KQ halves per row) |
   // sweep order (int32 per V row) | bucket counts / cursors | scaled row norms in
-  // sweep order (fp32 per V row)
+  // sweep order (fp32 per V row) | 16 < top <= 128: per-row key logs
   return 256 + tk_table_bytes(n_v, k) + 2 * align_up(4 * (size_t)(n_v > 0 ? n_v : 0)) +
-         align_up(4 * (size_t)kTkBuckets);
+         align_up(4 * (size_t)kTkBuckets) + tk_log_bytes(n_q, k, top);
 }
 
 int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t ld, int32_t k,
@@ -1132,6 +1229,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   int32_t* perm = reinterpret_cast<int32_t*>(static_cast<char*>(ws) + 256 + tk_table_bytes(n_v, k));
   int32_t* hist = perm + align_up(4 * (size_t)n_v) / 4;
   float* vnorm = reinterpret_cast<float*>(hist + align_up(4 * (size_t)kTkBuckets) / 4);
+  uint64_t* tlog = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(vnorm) +
+                                               align_up(4 * (size_t)(n_v > 0 ? n_v : 0)));
   const int kq = topk_kq(k);
   const int kq_shift = __builtin_ctz(kq);
   ALS_HIP(hipMemsetAsync(scal_u, 0, 2 * sizeof(unsigned), st));
@@ -1162,17 +1261,25 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   }
   const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
   const int nw = topk_nw(top, quad, rg);  // wavefronts per workgroup
-  const unsigned grid = (unsigned)((n_q + 16 * nw * rg - 1) / (16 * nw * rg));
+  const int64_t rows_blk = 16 * (int64_t)nw * rg;
+  const int64_t n_blk = (n_q + rows_blk - 1) / rows_blk;
+  // quad lists: launches of at most kTkLogBlocks blocks (one log slab per block)
+  const int64_t blk_per = quad ? (int64_t)kTkLogBlocks : n_blk;
   const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
   const uint4* vlo4 = vsp4 + n_v * (kq / 8);  // lo plane
 #define ALS_TOPK_SPLIT_LAUNCH2(NK, RG, TR)                                                      \
   do {                                                                                          \
     ALS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&topk_split_kernel<NK, RG, TR>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));         \
-    topk_split_kernel<NK, RG, TR><<<grid, 64 * nw, lds, st>>>(Q, n_q, vsp4, vlo4, perm, vnorm,   \
-                                                          n_v, ld, k, top, scal, idx_out,       \
-                                                          score_out);                           \
-    ALS_LAUNCH_CHECK();                                                                         \
+    for (int64_t b0 = 0; b0 < n_blk; b0 += blk_per) {                                           \
+      const int64_t r0 = b0 * rows_blk;                                                         \
+      const int64_t nq_c = std::min<int64_t>(n_q - r0, blk_per * rows_blk);                     \
+      const unsigned grid = (unsigned)((nq_c + rows_blk - 1) / rows_blk);                       \
+      topk_split_kernel<NK, RG, TR><<<grid, 64 * nw, lds, st>>>(                                \
+          Q + r0 * ld, nq_c, vsp4, vlo4, perm, vnorm, n_v, ld, k, top, scal, idx_out + r0 * top, \
+          score_out + r0 * top, tlog);                                                          \
+      ALS_LAUNCH_CHECK();                                                                       \
+    }                                                                                           \
   } while (0)
 #define ALS_TOPK_SPLIT_LAUNCH(NK, RG)                 \
   do {                                                \
@@ -1184,16 +1291,14 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
     else if (!quad)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
-    else if (rg != 1)                                 \
-      return ALS_EUNSUPPORTED;                        \
     else if (top <= 32)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 32);              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 32);             \
     else if (top <= 64)                               \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 64);              \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 64);             \
     else if (top <= 100)                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, 100);             \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 100);            \
     else                                              \
-      ALS_TOPK_SPLIT_LAUNCH2(NK, 1, kTopQ);           \
+      ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopQ);          \
   } while (0)
   if (kq == 32) {
     if (rg == 2) ALS_TOPK_SPLIT_LAUNCH(1, 2);

@@ -807,6 +807,48 @@ def test_topk_zero_rows_and_norm_order_ties(rank, top):
         assert list(idx[row]) == list(range(top)) and np.all(sc[row] == 0)
 
 
+@pytest.mark.parametrize("rank,top", [(32, 20), (64, 100), (128, 100), (128, 128)])
+def test_topk_log_overflow_exact_ties(rank, top):
+    """16 < top <= 128 keeps each row's keys in a log of 1,024 (csrc/topk.hip
+    kTkLogCap): every key reaching the row's running k-th score is appended, ties
+    included.  3,000 exact copies of one strong V row tie for every query that scores it
+    high: in every row that lists a copy, all 3,000 copies reach the running k-th score
+    and the log, which overflows and is cut to the row's `top` best keys mid-sweep (the
+    index decides among the copies), several times: the listed copies must be exactly
+    the lowest-index ones, in index order, after every better-scoring row."""
+    rng = np.random.default_rng(rank + top + 11)
+    n_q, n_v, n_copy = 200, 6000, 3000
+    Q = rng.standard_normal((n_q, rank)).astype(np.float32)
+    Vm = rng.standard_normal((n_v, rank)).astype(np.float32)
+    copies = np.sort(rng.choice(n_v, n_copy, replace=False))
+    Vm[copies] = 3.0 * Vm[copies[0]]  # one strong row, 3,000 times
+    ld = E.ld_for(rank)
+    Qd = torch.zeros((n_q, ld), device=DEV)
+    Qd[:, :rank] = torch.as_tensor(Q).to(DEV)
+    Vd = torch.zeros((n_v, ld), device=DEV)
+    Vd[:, :rank] = torch.as_tensor(Vm).to(DEV)
+    idx, sc = E.topk_rows(Qd, n_q, Vd, n_v, rank, top)
+    idx, sc = idx.cpu().numpy(), sc.cpu().numpy()
+    ref_i, ref_s = O.topk(Q, Vm, top)
+    S = Q.astype(np.float64) @ Vm.astype(np.float64).T
+    is_copy = np.zeros(n_v, bool)
+    is_copy[copies] = True
+    with_copies = 0
+    for row in range(n_q):
+        got = idx[row]
+        listed = got[is_copy[got]]
+        # the copies listed are the lowest-index ones, in index order
+        np.testing.assert_array_equal(listed, copies[:len(listed)])
+        np.testing.assert_array_equal(listed, ref_i[row][is_copy[ref_i[row]]])
+        if not np.array_equal(got, ref_i[row]):
+            for p_ in np.nonzero(got != ref_i[row])[0]:
+                assert abs(S[row, got[p_]] - ref_s[row, p_]) <= 1e-5 * max(1, abs(ref_s[row, p_]))
+        np.testing.assert_allclose(sc[row], ref_s[row], rtol=1e-5, atol=1e-5)
+        # a listed copy scores >= the row's k-th: all 3,000 copies reached the log
+        with_copies += len(listed) > 0
+    assert with_copies > 20
+
+
 @pytest.mark.parametrize("rank,top", [(32, 20), (128, 100), (64, 200)])
 def test_topk_large_v_lds_lists(rank, top):
     """More than 2^18 V rows (many tall quad-list tiles, a ragged last one), as at configs[4]."""

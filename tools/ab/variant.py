@@ -38,6 +38,12 @@ __device__ __forceinline__ float sel_lane16_n(float v, float w) {
 
 VARIANTS = {
     "base": [],
+    # round 6: quad top-k lists (16 < top <= 128) with one row group only
+    # round 6: the committed (HEAD) topk.hip in place of the working tree's ("@HEAD" files)
+    "oldtopk": [(TK, "@HEAD", None)],
+    # round 6: the LDL^T pivot-spread limit (rows beyond it go to the fp64 rescue)
+    **{f"cond{c}": [(GS, "constexpr float kCondMax = 32.f;", f"constexpr float kCondMax = {c}.f;")]
+       for c in (2, 4, 8, 16)},
     # the round-4 rescue guards off: no split-window / rank-deficiency tests, no
     # pivot-spread test (timing only: rows that need the rescue are then wrong)
     "noguard": [
@@ -291,6 +297,12 @@ def build(tag: str) -> str:
     shutil.copytree(CSRC, src)
     for f, old, new in VARIANTS[tag]:
         p = os.path.join(src, f)
+        if old == "@HEAD":  # the whole file as committed
+            rel = "recommender-system-using-apache-spark-mllib-_amd/csrc/" + f
+            open(p, "w").write(subprocess.check_output(["git", "show", "HEAD:" + rel],
+                                                       cwd=os.path.join(HERE, "..", ".."),
+                                                       text=True))
+            continue
         s = open(p).read()
         if old not in s:
             raise SystemExit(f"{tag}: patch does not apply to {f}: {old[:70]!r}")

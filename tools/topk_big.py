@@ -52,13 +52,15 @@ def main():
         if cnt:
             L.als_dev_tk_counters(buf, 1)
             print(f"  counters per call: {[v // 2 for v in buf[:5]]}", flush=True)
+    keep = 1 << 20  # rows saved / compared (all rows would be 8.8 GB at 10M users)
     if os.environ.get("TOPK_SAVE"):
-        torch.save({t: tuple(x.cpu() for x in r) for t, r in res.items()}, os.environ["TOPK_SAVE"])
+        torch.save({t: tuple(x[:keep].cpu() for x in r) for t, r in res.items()},
+                   os.environ["TOPK_SAVE"])
     if os.environ.get("TOPK_CMP"):
         ref = torch.load(os.environ["TOPK_CMP"], weights_only=True)
         for t, r in res.items():
             i0, s0 = ref[t]
-            i1, s1 = (x.cpu() for x in r)
+            i1, s1 = (x[:keep].cpu() for x in r)
             print(f"{lib} top{t}: index agreement {float((i0 == i1).float().mean()):.7f} "
                   f"max|dscore| {float((s0 - s1).abs().max()):.3e}", flush=True)
 

@@ -319,15 +319,18 @@ def topk_variant(k: int, top: int, n_q: int):
     """The kernel als_topk launches (csrc/topk.hip) and its grid in threads:
     (<NK, row groups, list kind>, grid)."""
     nk = max(32, kp_of(k)) // 32
-    if top <= 16:  # two row groups from 4 x 256 x 256 query rows (topk_split_rg)
-        rg, tr = (2 if n_q >= 4 * 256 * 256 else 1), (8 if top <= 8 else (12 if top <= 12 else 16))
-    elif top <= 128:  # quad register lists, one row group
-        rg, tr = 1, (32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128)))
+    rg = 2 if n_q >= 4 * 256 * 256 else 1  # two row groups from 4 x 256 x 256 query rows
+    if top <= 16:  # register lists (topk_split_rg)
+        tr = 8 if top <= 8 else (12 if top <= 12 else 16)
+    elif top <= 128:  # key logs, launched in chunks of <= 512 blocks (kTkLogBlocks)
+        tr = 32 if top <= 32 else (64 if top <= 64 else (100 if top <= 100 else 128))
     else:
         return f"topk_split_kernel<{nk},?,0>", None
-    nw = 8  # wavefronts per workgroup with register lists (tk_nw)
-    grid = (n_q + 16 * nw * rg - 1) // (16 * nw * rg) * 64 * nw
-    return f"topk_split_kernel<{nk},{rg},{tr}>", grid
+    nw = 8  # wavefronts per workgroup with register lists / key logs (tk_nw)
+    blocks = (n_q + 16 * nw * rg - 1) // (16 * nw * rg)
+    if top > 16:
+        blocks = min(blocks, 512)  # the grid of every launch but the last
+    return f"topk_split_kernel<{nk},{rg},{tr}>", blocks * 64 * nw
 
 
 def topk_roofline(workload: str, n_q: int, n_v: int, k: int, ms: float, top: int):

@@ -425,14 +425,12 @@ __global__ __launch_bounds__(256) void topk_split_table_kernel(const float* __re
 // LDS (one ds_write_b128 per lane); each owner lane takes its row's survivors
 // from the ballots, inserts them, and the new k-th scores go back to the
 // filtering lanes through LDS.  16 < top <= 128 (TOPR = 32 / 64 / 100 / 128, one
-// row group): quad lists — a row's running top scores are split over its four lanes
-// 16j + rho as sorted sub-lists of TOPR / 4 scores; the row's k-th best is the least
-// of their four minima (two lane swaps), a better score replaces that minimum in the
-// lane holding it, and every row of the wave inserts in the same pass (the LDS path
-// below inserts one candidate per wave at a time: 70 ms vs 13.6 ms of scores at
-// rank 128 top 100 on the ML-25M shape).  Every key reaching the k-th score (ties
-// included) is appended to the row's log in global memory; the output is the exact
-// top `top` keys of the log (tk_log_kth), ranked.
+// row groups as top <= 16): key logs — no list in registers; every key reaching its
+// row's threshold (the exact k-th best score as of the last cut of the row's log) is
+// appended to the log, one ballot per row and block (the LDS path below inserts one
+// candidate per wave at a time: 70 ms vs 13.6 ms of scores at rank 128 top 100 on the
+// ML-25M shape); the output is the exact top `top` keys of the log (tk_log_kth),
+// ranked.
 // TOPR = 0 (top > 128): sorted lists in LDS, wave-cooperative insertion
 // (topk_offer), 4 wavefronts.
 // Tile rows (hi halves only, RW = 4 NK uint4 per row): register lists (8
@@ -477,79 +475,74 @@ __device__ __forceinline__ void tk_insert(uint64_t (&kv)[TOPR], uint64_t c) {
   }
 }
 
-// Quad lists (16 < top <= 128, one row group per workgroup): row rho of a wave is
-// owned by its four lanes 16j + rho, each holding a sorted sub-list of S = TOPR / 4
-// SCORES (sub-list j has top / 4 (+1 for j < top % 4) live slots, +inf sentinels
-// above, -inf while open).  The union is the row's running top scores; its k-th best
-// is the smallest [0] of the four, found by two row swaps.  A better score replaces
-// that minimum in the lane that holds it (tk_insert_f drops [0]), so the sub-list
-// sizes never change; the rows of a wave insert in parallel, one candidate per row per
-// pass.  The (score, index) keys themselves go to the row's log (below); round 5 kept
-// the 64-bit keys in the sub-lists (224 registers, configs[4] sample top-100 191 ms,
-// vs 198 registers and 177 ms now: profiles/r06/ab_topk_logs.txt).
-
-// Value of x in lane (j ^ 1, rho) (X = 16) or (j ^ 2, rho) (X = 32), j = lane / 16.
-template <int X>
-__device__ __forceinline__ uint32_t tk_partner(uint32_t x) {
-  uint32_t a = x, b = x;
-  if constexpr (X == 16)
-    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
-  else
-    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
-  // rows j and j ^ (X / 16) exchanged: a holds the lower row of the pair, b the upper
-  const int j = (threadIdx.x & 63) >> 4;
-  return (j & (X / 16)) ? a : b;
+// Per-row key logs (16 < top <= 128).  No list lives in registers: every (score, index)
+// key that reaches its row's threshold is appended to the row's log in global memory
+// (tk_log_cap keys per row), the 16 lanes of a row group placing a block's keys with one
+// ballot per row.  The threshold is the row's exact k-th best score as of the last cut
+// of its log: a log that one more tile could overflow is cut in place to its `top`
+// largest keys (tk_log_kth), whose smallest then becomes the threshold, and at the end
+// of the sweep the row's output is selected from its log the same way.  Every key that
+// ranks above the running k-th has reached the log, because the threshold never
+// exceeds it, so the cuts and the output are exact.
+// (384 vs 512 vs 1,024 keys at rank 128: the configs[4] sample's top-100 144 / 146 / 162 ms,
+// profiles/r06/ab_topk_logs.txt)
+constexpr int kTkLogCapMin = 384;
+// Keys per row log of a kernel: at least kTkLogCapMin and room for `top` keys plus one
+// tile's worth (a log is cut when the next tile could overflow it), in 64-key steps.
+__host__ __device__ constexpr int tk_log_cap(int nk, int topr) {
+  return ((topr + tk_vt(nk, 1) > kTkLogCapMin ? topr + tk_vt(nk, 1) : kTkLogCapMin) + 63) / 64 * 64;
 }
-// Smallest score over the four lanes of this lane's row.
-__device__ __forceinline__ float tk_quad_minf(float x) {
-  x = fminf(x, __uint_as_float(tk_partner<16>(__float_as_uint(x))));
-  return fminf(x, __uint_as_float(tk_partner<32>(__float_as_uint(x))));
-}
-
-// Insert score c into a sorted ascending score sub-list (its least at [0], +inf
-// sentinels past the live slots), dropping [0]; the caller has checked c > [0].
-template <int N>
-__device__ __forceinline__ void tk_insert_f(float (&sv)[N], float c) {
-  bool gt[N + 1];
-#pragma unroll
-  for (int j = 0; j < N; ++j) gt[j] = c > sv[j];
-  gt[N] = false;
-#pragma unroll
-  for (int j = 0; j < N; ++j) {
-    const float nx = j + 1 < N ? sv[j + 1] : 0.f;
-    sv[j] = gt[j + 1] ? nx : (gt[j] ? c : sv[j]);
-  }
-}
-
-// Per-row key logs (16 < top <= 128).  Every (score, index) key that reaches its row's
-// running top is appended to the row's log in global memory (kTkLogCap keys per row);
-// the registers keep only the scores (the quad sub-lists above), which is all the
-// filter needs.  At the end of the sweep the row's `top` largest keys are selected from
-// its log exactly (tk_log_select), and a log about to overflow is compacted to them.
-constexpr int kTkLogCap = 1024;
-constexpr int kTkLogJ = kTkLogCap / 64;  // keys per lane when a wave holds a whole log
 // Query-row blocks per launch with logs (one log slab per block of a launch: at most
-// 512 x 128 rows x 8 KB = 512 MB; a larger n_q runs in launches of this many blocks).
+// 512 x 256 rows x 384 keys x 8 B = 403 MB at rank 128; a larger n_q runs in launches of
+// this many blocks).
 // All 10M users of configs[4], top-100: 6,733 ms with 512-block launches, 6,750 ms
 // with 4096 (profiles/r06/ab_topk_logs.txt).  (A grid-stride loop over the blocks
 // inside the kernel instead took every top-k kernel's registers to the 256 limit and
 // spilled: not used.)
 constexpr int kTkLogBlocks = 512;
 
-// The T-th largest of the n keys of log L (n <= kTkLogCap, 1 <= T <= n), by a bitwise
-// search over the 64 key bits: the largest P with #{keys >= P} >= T.  Keys are unique
-// ((score, V row) pairs), so exactly T keys are >= P.  The wave's lanes hold the keys
-// (kv[j] = L[64 j + lane], 0 past n: below every real key).
-__device__ __forceinline__ uint64_t tk_log_kth(const uint64_t (&kv)[kTkLogJ], int T) {
-  uint64_t P = 0;
-  for (int b = 63; b >= 0; --b) {
-    const uint64_t cand = P | (1ull << b);
+// The T-th largest of the n keys of log L (n <= 64 J, 1 <= T <= n): the largest P
+// with #{keys >= P} >= T.  Keys are unique ((score, V row) pairs), so exactly T keys are
+// >= P.  The wave's lanes hold the keys (kv[j] = L[64 j + lane], 0 past n: below every
+// real key).  A bitwise search over the 32 score bits first (the T-th largest score S);
+// when the keys scoring S are exactly the ones still needed, P is the least of them (a
+// min over the wave); only with more ties at S than needed does a second bitwise search
+// over the index bits of those keys run.
+template <int J>
+__device__ __forceinline__ uint64_t tk_log_kth(const uint64_t (&kv)[J], int T) {
+  uint32_t S = 0;
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t cand = S | (1u << b);
     int c = 0;
 #pragma unroll
-    for (int j = 0; j < kTkLogJ; ++j) c += __popcll(__ballot(kv[j] >= cand));
-    if (c >= T) P = cand;
+    for (int j = 0; j < J; ++j) c += __popcll(__ballot((uint32_t)(kv[j] >> 32) >= cand));
+    if (c >= T) S = cand;
   }
-  return P;
+  int gt = 0, eq = 0;
+  uint32_t lmin = 0xFFFFFFFFu;
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const uint32_t h = (uint32_t)(kv[j] >> 32);
+    gt += __popcll(__ballot(h > S));
+    eq += __popcll(__ballot(h == S));
+    if (h == S) lmin = min(lmin, (uint32_t)kv[j]);
+  }
+  const int need = T - gt;  // 1 <= need <= eq
+  if (need == eq) {  // every key scoring S is kept: P is the least of them
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lmin = min(lmin, (uint32_t)__shfl_xor((int)lmin, o));
+    return ((uint64_t)S << 32) | lmin;
+  }
+  uint32_t L = 0;  // the need-th largest index word among the keys scoring S
+  for (int b = 31; b >= 0; --b) {
+    const uint32_t cand = L | (1u << b);
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      c += __popcll(__ballot((uint32_t)(kv[j] >> 32) == S && (uint32_t)kv[j] >= cand));
+    if (c >= need) L = cand;
+  }
+  return ((uint64_t)S << 32) | L;
 }
 
 // Wavefronts per workgroup: 8 with register lists (each V tile feeds 128 RG query
@@ -651,47 +644,56 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   float* thr = sblk + NW * RG * 256 + w * RG * 16;  // TOPR > 0: [g][row] k-th scores
   if (TOPR > 0 && lane < 16 * RG)
     thr[lane] = ((live[lane >> 4] >> (lane & 15)) & 1u) ? -__builtin_inff() : __builtin_inff();
-  bool full = false;  // TOPR == 0: all 16 RG lists of this wave hold `top` entries
-  // TOPR > 0: this lane's row list (owner lanes lane < 16 RG), or (QUAD) its score
-  // sub-list of row m (every lane: sub-list q of each row group) with the row's keys
-  // in its log (tlog)
-  constexpr bool QUAD = TOPR > 16;
-  static_assert(!QUAD || TOPR % 4 == 0, "quad lists: TOPR / 4 per lane");
-  // (TOPR = 100: sub-lists of 25, sized for the top-100 of BASELINE configs[4])
-  constexpr int NR = TOPR > 0 ? (QUAD ? TOPR / 4 : TOPR) : 1;
-  constexpr int KG = QUAD ? RG : 1;  // quad: one sub-list per row group in every lane
-  const int ncap = QUAD ? top / 4 + (q < top % 4 ? 1 : 0) : top;  // live slots of this list
-  uint64_t kv[QUAD ? 1 : KG][QUAD ? 1 : NR];
-  float sv[QUAD ? KG : 1][QUAD ? NR : 1];
-  int lcnt[QUAD ? KG : 1];  // QUAD: keys in row m's log (the same in its four lanes)
-  if constexpr (QUAD) {
+  // TOPR <= 16: this lane's row list (owner lanes lane < 16 RG).  LOGS (16 < TOPR): no
+  // list in registers — every key reaching its row's threshold goes to the row's log
+  // (tlog), and the threshold is the row's exact k-th best score as of the last cut of
+  // its log (below)
+  constexpr bool LOGS = TOPR > 16;
+  constexpr int LCAP = tk_log_cap(NK, TOPR);  // LOGS: keys per row log
+  constexpr int LJ = LCAP / 64;               // ... per lane when a wave holds a whole log
+  static_assert(!LOGS || LCAP >= TOPR + VT, "a log holds top + one tile of keys");
+  // TOPR == 0: all 16 RG lists of this wave hold `top` entries; LOGS: always true (a row
+  // without a threshold yet has -inf, which the coarse test passes)
+  bool full = LOGS;
+  constexpr int NR = TOPR > 0 ? (LOGS ? 1 : TOPR) : 1;
+  constexpr int KG = LOGS ? RG : 1;
+  uint64_t kv[LOGS ? 1 : KG][LOGS ? 1 : NR];
+  // LOGS: keys in the log of row 4q + r of group g, and that row's exact threshold (its
+  // k-th best score at the last cut of its log; -inf before, +inf for dead rows): the
+  // same in the 16 lanes of row group q
+  int lcnt[LOGS ? KG : 1][LOGS ? 4 : 1];
+  float tx[LOGS ? KG : 1][LOGS ? 4 : 1];
+  if constexpr (LOGS) {
 #pragma unroll
-    for (int g = 0; g < KG; ++g) {
-      lcnt[g] = 0;
+    for (int g = 0; g < KG; ++g)
 #pragma unroll
-      for (int j = 0; j < NR; ++j) sv[g][j] = j < ncap ? -__builtin_inff() : __builtin_inff();
-    }
+      for (int r = 0; r < 4; ++r) {
+        lcnt[g][r] = 0;
+        tx[g][r] = ts[g][r];
+      }
   } else {
 #pragma unroll
     for (int g = 0; g < KG; ++g)
 #pragma unroll
-      for (int j = 0; j < NR; ++j) kv[g][j] = j < ncap ? kTkKeyOpen : kTkKeySentinel;
+      for (int j = 0; j < NR; ++j) kv[g][j] = j < top ? kTkKeyOpen : kTkKeySentinel;
   }
-  // QUAD: row (group g, row rho of this wave)'s log: kTkLogCap keys in this block's slab
+  // LOGS: row (group g, row rho of this wave)'s log: LCAP keys in this block's slab
   auto rowlog = [&](int g, int rho) -> uint64_t* {
-    return tlog + ((int64_t)blockIdx.x * GR * RG + GR * g + 16 * w + rho) * kTkLogCap;
+    return tlog + ((int64_t)blockIdx.x * GR * RG + GR * g + 16 * w + rho) * LCAP;
   };
-  // QUAD: keep the `top` largest keys of row (g, rho)'s log (n > top keys), in place
-  auto log_compact = [&](int g, int rho, int n) {
+  // LOGS: keep the `top` largest keys of row (g, rho)'s log (n > top keys), in place;
+  // returns the score of the `top`-th (the row's exact k-th best so far: every key that
+  // could rank above it reached the log, since the threshold never exceeded it)
+  auto log_compact = [&](int g, int rho, int n) -> float {
     uint64_t* L = rowlog(g, rho);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's appends have landed
-    uint64_t kl[kTkLogJ];
+    uint64_t kl[LJ];
 #pragma unroll
-    for (int j = 0; j < kTkLogJ; ++j) kl[j] = 64 * j + lane < n ? L[64 * j + lane] : 0ull;
+    for (int j = 0; j < LJ; ++j) kl[j] = 64 * j + lane < n ? L[64 * j + lane] : 0ull;
     const uint64_t P = tk_log_kth(kl, top);
     int base = 0;
 #pragma unroll
-    for (int j = 0; j < kTkLogJ; ++j) {
+    for (int j = 0; j < LJ; ++j) {
       const bool kp = kl[j] >= P;
       const uint64_t b = __ballot(kp);
       const int pos = base + __popcll(b & ((1ull << lane) - 1));
@@ -699,6 +701,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       base += __popcll(b);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return tk_key_score(P);
   };
 
   // Tile staging by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write): the
@@ -730,7 +733,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   float nv_cur = 0.f;
   // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m (reading
   // the B operands one block ahead in registers measured no faster: the sweep is not
-  // bound by LDS latency, and the quad kernel then spills)
+  // bound by LDS latency, and the round-5 quad-list kernel then spilled)
   auto score = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG]) {  // hi.hi
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -780,15 +783,41 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       const floatx4 t4 = *reinterpret_cast<const floatx4*>(thr + 16 * g + 4 * q);
       const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ts[g][r] = ((live[g] >> (4 * q + r)) & 1u) ? fmaf(-s4[r], nvt, t4[r]) : __builtin_inff();
+      for (int r = 0; r < 4; ++r) {
+        const bool lv = (live[g] >> (4 * q + r)) & 1u;
+        ts[g][r] = lv ? fmaf(-s4[r], nvt, t4[r]) : __builtin_inff();
+        if constexpr (LOGS) tx[g][r] = lv ? t4[r] : __builtin_inff();
+      }
     }
   };
   // acc: hi.hi scores of the block (refined in place when it passes the coarse
   // filter); tbr: the block's B rows in the tile
   auto filter = [&](floatx4 (&acc)[RG], int64_t ibase, const int* bperm, const uint4* tbr) {
     // acc[g][r] = scaled score(row GR g + 16w + 4q + r, V row ibase + m)
-    if constexpr (TOPR > 0) {
+    if constexpr (LOGS) {
+      // coarse: hi.hi >= the coarse threshold; then every exact score at or above its
+      // row's threshold goes to the row's log, the 16 lanes of a row group placing
+      // their keys by one ballot per row (no per-candidate pass).  Rows past n_v score
+      // NaN and dead rows have +inf thresholds: nothing of theirs is appended.
+      bool c = false;
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= ts[g][r];
+      if (__ballot(c) == 0) return;
+      refine(tbr, ibase, acc);
+      const unsigned below = (1u << m) - 1u;
+#pragma unroll
+      for (int g = 0; g < RG; ++g)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool ok = acc[g][r] >= tx[g][r];
+          const unsigned grp = (unsigned)(__ballot(ok) >> (16 * q)) & 0xFFFFu;
+          if (ok) rowlog(g, 4 * q + r)[lcnt[g][r] + __popc(grp & below)] = tk_key(acc[g][r], bperm[m]);
+          lcnt[g][r] += __popc(grp);
+        }
+      return;
+    } else if constexpr (TOPR > 0) {
       // coarse: hi.hi >= the coarse threshold; then the exact scores go to the
       // owners against the same threshold (a weaker test than the k-th score: the
       // owner lanes compare exact (score, index) keys); until the lists are full
@@ -818,50 +847,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
         for (int r = 0; r < 4; ++r) b[g][r] = __ballot(pr[g][r]);
       }
       asm volatile("" ::: "memory");  // LDS is in order within the wave
-      if constexpr (QUAD) {
-        // every lane: sub-list q of row m of each group; one candidate per row and
-        // group per pass
-        const int rho = m;
-        unsigned msk[KG];
-#pragma unroll
-        for (int g = 0; g < KG; ++g) {
-          // this row's ballot among the four (wave-uniform) ones: masked merges, the
-          // masks opaque to the compiler (a select chain on a lane-varying index is
-          // otherwise turned into a private-memory table lookup)
-          uint64_t bb = b[g][0];
-#pragma unroll
-          for (int t = 1; t < 4; ++t) {
-            uint64_t sel = (rho & 3) == t ? ~0ull : 0ull;
-            asm volatile("" : "+v"(sel));
-            bb = (bb & ~sel) | (b[g][t] & sel);
-          }
-          msk[g] = (unsigned)(bb >> (16 * (rho >> 2))) & 0xFFFFu;
-        }
-        auto pass = [&](int g) {
-          const bool act = msk[g] != 0;
-          const int mm = act ? __builtin_ctz(msk[g]) : 0;
-          msk[g] &= msk[g] - 1;
-          const float sc = st[g * 256 + rho + 16 * mm];
-          const float gmin = tk_quad_minf(sv[g][0]);
-          // the lowest sub-list whose [0] is the row minimum takes a better score
-          const uint64_t holders = (__ballot(sv[g][0] == gmin) >> rho) & 0x0001000100010001ull;
-          // the four lanes of row rho agree: a score reaching the row's running
-          // k-th (ties included: the index decides at the end) goes to the log
-          if (act && sc == sc && sc >= gmin) {
-            if (q == 0) rowlog(g, rho)[lcnt[g]] = tk_key(sc, bperm[mm]);
-            lcnt[g] += 1;
-            if (sc > gmin && q == (__builtin_ctzll(holders) >> 4)) tk_insert_f<NR>(sv[g], sc);
-          }
-        };
-#pragma unroll
-        for (int g = 0; g < KG; ++g)
-          while (__ballot(msk[g] != 0)) pass(g);
-#pragma unroll
-        for (int g = 0; g < KG; ++g) {
-          const float gmin = tk_quad_minf(sv[g][0]);
-          if (q == 0) thr[16 * g + rho] = gmin;  // -inf while the row has open slots
-        }
-      } else if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
+      if (lane < 16 * RG) {  // owner lanes: group g = lane / 16, row rho
         const int g = lane >> 4, rho = lane & 15, sel = 4 * g + (rho & 3);
         uint64_t bb = b[0][0];
 #pragma unroll
@@ -880,15 +866,8 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       asm volatile("" ::: "memory");
       refresh();
       if (!full) {
-        bool open_list = false;
-        if constexpr (QUAD) {
-#pragma unroll
-          for (int g = 0; g < KG; ++g)
-            open_list = open_list || (((live[g] >> m) & 1u) && lcnt[g] < top);
-        } else {
-          open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
-                      kv[0][0] == kTkKeyOpen;
-        }
+        const bool open_list = lane < 16 * RG && ((live[lane >> 4] >> (lane & 15)) & 1u) &&
+                               kv[0][0] == kTkKeyOpen;
         full = __ballot(open_list) == 0;
       }
       return;
@@ -938,19 +917,28 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   // buffer buf; false: sweep over
   auto tile_step = [&](int64_t vb) -> bool {
       const uint4* tb = tiles + buf * VT * RW;
-      if constexpr (QUAD) {
+      if constexpr (LOGS) {
         // a log that this tile could overflow (at most VT appends per row) is cut to
-        // its row's `top` best keys first
+        // its row's `top` best keys first, and the row's threshold rises to the k-th of
+        // them (refresh() below reads it)
 #pragma unroll
-        for (int g = 0; g < KG; ++g) {
-          uint64_t nb = __ballot(q == 0 && lcnt[g] > kTkLogCap - VT) & 0xFFFFull;
-          while (nb) {
-            const int rho = __builtin_ctzll(nb);
-            nb &= nb - 1;
-            log_compact(g, rho, __builtin_amdgcn_readlane(lcnt[g], rho));
-            if (m == rho) lcnt[g] = top;
+        for (int g = 0; g < KG; ++g)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // (cutting more often — at top + 32 / 64 / 128 keys, or as soon as a row
+            // first holds `top` — measured slower: the cuts cost more than the fresher
+            // thresholds save; profiles/r06/ab_topk_logs.txt)
+            uint64_t nb = __ballot(m == 0 && lcnt[g][r] > LCAP - VT);
+            while (nb) {
+              const int L0 = __builtin_ctzll(nb);  // lane 16 qq: row 4 qq + r
+              nb &= nb - 1;
+              const int rho = 4 * (L0 >> 4) + r;
+              const float t = log_compact(g, rho, __builtin_amdgcn_readlane(lcnt[g][r], L0));
+              if (lane == 0) thr[16 * g + rho] = t;
+              if (q == (L0 >> 4)) lcnt[g][r] = top;
+            }
           }
-        }
+        asm volatile("" ::: "memory");  // the thresholds are read back below (LDS in order)
       }
       nv_cur = n_v > 0 ? vnorm[vb] : 0.f;
       nvt = fmaf(nv_cur, 1.01f, 1.f);
@@ -1041,7 +1029,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
     if (!tile_step(vb)) break;
   // no LDS-DMA may still be landing when the workgroup ends
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (QUAD) {
+  if constexpr (LOGS) {
     // each row's `top` largest keys, selected exactly from its log, ranked and written
     // in order; fewer than `top` keys (n_v < top) leave the tail open
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's log appends landed
@@ -1059,16 +1047,18 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
           }
           continue;
         }
-        const int n = __builtin_amdgcn_readlane(lcnt[g], rho);
+        const int rq = rho & 3;
+        const int cr = rq == 0 ? lcnt[g][0] : (rq == 1 ? lcnt[g][1] : (rq == 2 ? lcnt[g][2] : lcnt[g][3]));
+        const int n = __builtin_amdgcn_readlane(cr, 16 * (rho >> 2));
         const uint64_t* L = rowlog(g, rho);
-        uint64_t kl[kTkLogJ];
+        uint64_t kl[LJ];
 #pragma unroll
-        for (int j = 0; j < kTkLogJ; ++j) kl[j] = 64 * j + lane < n ? L[64 * j + lane] : 0ull;
+        for (int j = 0; j < LJ; ++j) kl[j] = 64 * j + lane < n ? L[64 * j + lane] : 0ull;
         const int T = n < top ? n : top;
         const uint64_t P = n > top ? tk_log_kth(kl, T) : 1ull;  // real keys are >= 1
         int base = 0;
 #pragma unroll
-        for (int j = 0; j < kTkLogJ; ++j) {
+        for (int j = 0; j < LJ; ++j) {
           const bool kp = kl[j] >= P;
           const uint64_t b = __ballot(kp);
           if (kp) ks[base + __popcll(b & ((1ull << lane) - 1))] = kl[j];
@@ -1122,23 +1112,24 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
 static int topk_kq(int k) { return k <= 32 ? 32 : (k <= 64 ? 64 : 128); }
 
 constexpr int kTopR = 16;   // one owner lane's register list for top <= kTopR (sized 8 / 12 / 16)
-constexpr int kTopQ = 128;  // quad register lists for kTopR < top <= kTopQ (32 / 64 / 100 / 128)
+constexpr int kTopQ = 128;  // key logs for kTopR < top <= kTopQ (32 / 64 / 100 / 128)
 
-// Quad register lists for kTopR < top <= kTopQ.  Measured at rank 128, top 100
-// against the LDS lists: 59,047 V rows 70 -> 21 ms, 1,000,000 V rows 456 -> 330 ms.
-static bool topk_quad(int top, int64_t n_v) {
+// Key logs for kTopR < top <= kTopQ.  (Round 4's quad register lists measured at rank
+// 128, top 100 against the LDS lists: 59,047 V rows 70 -> 21 ms, 1,000,000 V rows 456 ->
+// 330 ms; the logs replaced them in round 6.)
+static bool topk_logs(int top, int64_t n_v) {
   (void)n_v;
   return top > kTopR && top <= kTopQ;
 }
 
-static int topk_nw(int top, bool quad, int rg) {
-  return quad ? tk_nw(kTopQ) : (top <= kTopR ? tk_nw(1) : tk_nw(0));
+static int topk_nw(int top, bool logs, int rg) {
+  return logs ? tk_nw(kTopQ) : (top <= kTopR ? tk_nw(1) : tk_nw(0));
 }
 
-static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
+static size_t topk_split_lds_bytes(int kq, int rg, int top, bool logs) {
   const int nk = kq / 32;
-  const int nw = topk_nw(top, quad, rg);
-  const bool reg_lists = top <= kTopR || quad;
+  const int nw = topk_nw(top, logs, rg);
+  const bool reg_lists = top <= kTopR || logs;
   const size_t vt = (size_t)tk_vt(nk, reg_lists ? 1 : 0);
   // [nbuf][vt] tile rows of KQ hi halves (kq/8 uint4) | [nbuf][max(vt, 64)] V rows |
   // [2][nw] done flags | [nw][rg][16] slack coefficients | [nw][nk][64] uint4 lo scratch
@@ -1160,14 +1151,12 @@ static size_t topk_split_lds_bytes(int kq, int rg, int top, bool quad) {
 // users, rank 64) 4.7 ms with two groups, 3.6 ms with one (the tail of 2.5 rounds);
 // configs[4] (262,144-user sample, rank 128) 97 ms with two, 151 ms with one.
 constexpr int64_t kTkRg2MinRows = 4 * 256 * 256;
-static int topk_split_rg(int k, int top, bool quad, int64_t n_q) {
+static int topk_split_rg(int k, int top, bool logs, int64_t n_q) {
   const int kq = topk_kq(k);
-  // quad lists (score sub-lists in registers, keys in per-row logs): one row group.
-  // (Round 6, configs[4] 262,144-user sample, top-100: one group 176.5 ms, two groups
-  // 212.7 ms — two groups' sub-lists and A operands exceed 256 registers, 50 spilled;
-  // round 5's 64-bit key lists: 190 ms.  profiles/r06/ab_topk_logs.txt)
-  if (quad) return 1;
-  if (top <= kTopR && n_q < kTkRg2MinRows) return 1;
+  // register lists and key logs: two row groups on the same condition (the logs keep
+  // no list in registers, so two groups' A operands and accumulators fit)
+  if ((top <= kTopR || logs) && n_q < kTkRg2MinRows) return 1;
+  if (logs) return 2;
   const size_t rg2_limit = top > kTopR ? (size_t)kLdsBytes / 2 : (size_t)kLdsBytes;
   if (topk_split_lds_bytes(kq, 2, top, false) <= rg2_limit) return 2;
   if (topk_split_lds_bytes(kq, 1, top, false) <= (size_t)kLdsBytes) return 1;
@@ -1184,14 +1173,16 @@ static size_t tk_table_bytes(int64_t n_v, int32_t k) {
   return align_up(4 * (size_t)topk_kq(k) * (size_t)(n_v > 0 ? n_v : 0));
 }
 
-// Per-row key logs of the quad lists (16 < top <= 128): kTkLogCap keys for every query
+// Per-row key logs (16 < top <= 128): tk_log_cap keys for every query
 // row of one launch's blocks (at most kTkLogBlocks blocks per launch).
 static size_t tk_log_bytes(int64_t n_q, int32_t k, int32_t top) {
-  if (n_q <= 0 || !topk_quad(top, 0)) return 0;
+  if (n_q <= 0 || !topk_logs(top, 0)) return 0;
   const int rg = topk_split_rg(k, top, true, n_q);
   const int64_t rows = 16 * (int64_t)tk_nw(kTopQ) * rg;  // query rows per block
   const int64_t blocks = std::min<int64_t>((n_q + rows - 1) / rows, kTkLogBlocks);
-  return align_up(sizeof(uint64_t) * (size_t)(blocks * rows) * kTkLogCap);
+  const int topr = top <= 32 ? 32 : (top <= 64 ? 64 : (top <= 100 ? 100 : kTopQ));
+  return align_up(sizeof(uint64_t) * (size_t)(blocks * rows) *
+                  (size_t)tk_log_cap(topk_kq(k) / 32, topr));
 }
 
 size_t als_topk_workspace_bytes(int64_t n_q, int64_t n_v, int32_t k, int32_t top) {
@@ -1214,8 +1205,8 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
   if (n_q == 0) return ALS_OK;
   ALS_REQUIRE(Q && V && idx_out && score_out, ALS_EINVAL, "als_topk: null pointer");
   hipStream_t st = as_stream(stream);
-  const bool quad = topk_quad(top, n_v);
-  const int rg = topk_split_rg(k, top, quad, n_q);
+  const bool logs = topk_logs(top, n_v);
+  const int rg = topk_split_rg(k, top, logs, n_q);
   ALS_REQUIRE(rg > 0, ALS_EUNSUPPORTED, "als_topk: top %d at rank %d does not fit the LDS", top,
               k);
   ALS_REQUIRE(ws != nullptr && ws_bytes >= als_topk_workspace_bytes(n_q, n_v, k, top),
@@ -1259,12 +1250,12 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
         V, n_v, ld, k, scal, perm, vnorm);
     ALS_LAUNCH_CHECK();
   }
-  const size_t lds = topk_split_lds_bytes(kq, rg, top, quad);
-  const int nw = topk_nw(top, quad, rg);  // wavefronts per workgroup
+  const size_t lds = topk_split_lds_bytes(kq, rg, top, logs);
+  const int nw = topk_nw(top, logs, rg);  // wavefronts per workgroup
   const int64_t rows_blk = 16 * (int64_t)nw * rg;
   const int64_t n_blk = (n_q + rows_blk - 1) / rows_blk;
-  // quad lists: launches of at most kTkLogBlocks blocks (one log slab per block)
-  const int64_t blk_per = quad ? (int64_t)kTkLogBlocks : n_blk;
+  // key logs: launches of at most kTkLogBlocks blocks (one log slab per block)
+  const int64_t blk_per = logs ? (int64_t)kTkLogBlocks : n_blk;
   const uint4* vsp4 = reinterpret_cast<const uint4*>(vsp);
   const uint4* vlo4 = vsp4 + n_v * (kq / 8);  // lo plane
 #define ALS_TOPK_SPLIT_LAUNCH2(NK, RG, TR)                                                      \
@@ -1289,7 +1280,7 @@ int als_topk(const float* Q, int64_t n_q, const float* V, int64_t n_v, int32_t l
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 12);             \
     else if (top <= kTopR)                            \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, kTopR);          \
-    else if (!quad)                                   \
+    else if (!logs)                                   \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 0);              \
     else if (top <= 32)                               \
       ALS_TOPK_SPLIT_LAUNCH2(NK, RG, 32);             \

@@ -77,7 +77,9 @@ def test_phase_counters_combine_by_grid(bench, monkeypatch):
 
 @pytest.mark.parametrize("k,top,n_q,kern,grid", [
     (128, 10, 10_000_000, "topk_split_kernel<4,2,12>", 39063 * 512),
-    (128, 100, 10_000_000, "topk_split_kernel<4,1,100>", 78125 * 512),
+    (128, 100, 10_000_000, "topk_split_kernel<4,2,100>", 512 * 512),
+    (64, 100, 162_541, "topk_split_kernel<2,1,100>", 512 * 512),
+    (64, 100, 20_000, "topk_split_kernel<2,1,100>", 157 * 512),
     (64, 10, 162_541, "topk_split_kernel<2,1,12>", 1270 * 512),
     (128, 10, 262_144, "topk_split_kernel<4,2,12>", 1024 * 512),
     (128, 10, 262_143, "topk_split_kernel<4,1,12>", 2048 * 512),

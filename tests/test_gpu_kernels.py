@@ -809,9 +809,9 @@ def test_topk_zero_rows_and_norm_order_ties(rank, top):
 
 @pytest.mark.parametrize("rank,top", [(32, 20), (64, 100), (128, 100), (128, 128)])
 def test_topk_log_overflow_exact_ties(rank, top):
-    """16 < top <= 128 keeps each row's keys in a log of 1,024 (csrc/topk.hip
-    kTkLogCap): every key reaching the row's running k-th score is appended, ties
-    included.  3,000 exact copies of one strong V row tie for every query that scores it
+    """16 < top <= 128 keeps each row's keys in a log (csrc/topk.hip kTkLogCap keys): every
+    key reaching the row's threshold is appended, ties included.  3,000 exact copies of
+    one strong V row tie for every query that scores it
     high: in every row that lists a copy, all 3,000 copies reach the running k-th score
     and the log, which overflows and is cut to the row's `top` best keys mid-sweep (the
     index decides among the copies), several times: the listed copies must be exactly

@@ -1034,7 +1034,9 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
     // in order; fewer than `top` keys (n_v < top) leave the tail open
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's log appends landed
     uint64_t* ks = reinterpret_cast<uint64_t*>(sblk + w * RG * 256);  // <= 128 keys (1 KB)
-#pragma unroll 1
+    // (g unrolled: a runtime index into lcnt / live would put those arrays in scratch
+    // memory for the whole kernel, a scratch round trip per tile of the sweep)
+#pragma unroll
     for (int g = 0; g < KG; ++g) {
 #pragma unroll 1
       for (int rho = 0; rho < 16; ++rho) {

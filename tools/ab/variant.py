@@ -138,6 +138,53 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
 }  // extern "C"
 """),
     ],
+    # top-k logs (round 6) timing bound (no lists: wrong results): the sweep alone, every
+    # quartet scored (V stream, LDS, MFMA, barriers), no block filtered
+    "tk_sweeponly": [
+        (TK, """            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
+            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {""",
+         """            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
+#pragma unroll
+            for (int j = 0; j < NB4; ++j)
+#pragma unroll
+              for (int g = 0; g < RG; ++g)
+                asm volatile("" :: "v"(a4[j][g][0]), "v"(a4[j][g][1]), "v"(a4[j][g][2]), "v"(a4[j][g][3]));
+            if (true) continue;
+            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {"""),
+    ],
+    # top-k logs event counters (dev): quartets scored / past the coarse ballot, blocks
+    # refined, keys appended, log cuts (als_dev_tk_counters)
+    "tk_count2": [
+        (TK, "namespace als {\n", "namespace als {\n__device__ unsigned long long tk_dbg[8];\n"),
+        (TK, "              if (__ballot(any) == 0) continue;",
+         """              if (lane == 0) atomicAdd(&tk_dbg[0], 1ull);
+              if (__ballot(any) != 0 && lane == 0) atomicAdd(&tk_dbg[1], 1ull);
+              if (__ballot(any) == 0) continue;"""),
+        (TK, """      if (__ballot(c) == 0) return;
+      refine(tbr, ibase, acc);
+      const unsigned below""", """      if (__ballot(c) == 0) return;
+      if (lane == 0) atomicAdd(&tk_dbg[2], 1ull);
+      refine(tbr, ibase, acc);
+      const unsigned below"""),
+        (TK, "          lcnt[g][r] += __popc(grp);",
+         """          lcnt[g][r] += __popc(grp);
+          if (m == 0 && grp) atomicAdd(&tk_dbg[3], (unsigned long long)__popc(grp));"""),
+        (TK, "              if (lane == 0) thr[16 * g + rho] = t;",
+         """              if (lane == 0) thr[16 * g + rho] = t;
+              if (lane == 0) atomicAdd(&tk_dbg[4], 1ull);"""),
+        (TK, "}  // extern \"C\"\n", """int als_dev_tk_counters(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(als::tk_dbg), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(als::tk_dbg), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+
+}  // extern "C"
+"""),
+    ],
     # top-k: 192-row tiles at rank > 64 (register / quad lists)
     "tk_vt192": [
         (TK, "return topr == 0 ? 64 / nk : (nk == 4 ? 128 : 256 / nk);",

@@ -37,7 +37,7 @@ def main():
         dm = re.sub(r"\(.*\)$", "", dm)
         print(f"{dm[:70]:70s} V{r.get('VGPRs', '?'):>4} A{r.get('AGPRs', '?'):>3} "
               f"occ {r.get('Occupancy [waves/SIMD]', '?')} vspill {r.get('VGPRs Spill', '?')} "
-              f"sspill {r.get('SGPRs Spill', '?')}")
+              f"sspill {r.get('SGPRs Spill', '?')} scratch {r.get('ScratchSize [bytes/lane]', '?')}")
 
 
 if __name__ == "__main__":

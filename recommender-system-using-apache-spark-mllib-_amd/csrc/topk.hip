@@ -734,7 +734,9 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
   // B operand: lane (q, m) holds dims 32s + 8q .. +7 of the block's V row m (reading
   // the B operands one block ahead in registers measured no faster: the sweep is not
   // bound by LDS latency, and the round-5 quad-list kernel then spilled)
-  auto score = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG]) {  // hi.hi
+  // (chk false: the caller masks rows past n_v itself — the quartet loop does it once per
+  // quartet of the last tile, which keeps a per-block branch off its MFMA stream)
+  auto score = [&](const uint4* tb, int64_t ibase, floatx4 (&acc)[RG], bool chk) {  // hi.hi
 #pragma unroll
     for (int g = 0; g < RG; ++g) acc[g] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -744,7 +746,7 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       for (int g = 0; g < RG; ++g)
         acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh, acc[g], 0, 0, 0);
     }
-    if (ibase + 16 > n_v) {  // the last tile: rows past n_v score NaN
+    if (chk && ibase + 16 > n_v) {  // the last tile: rows past n_v score NaN
       const bool past = ibase + m >= n_v;
 #pragma unroll
       for (int g = 0; g < RG; ++g)
@@ -799,12 +801,12 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       // row's threshold goes to the row's log, the 16 lanes of a row group placing
       // their keys by one ballot per row (no per-candidate pass).  Rows past n_v score
       // NaN and dead rows have +inf thresholds: nothing of theirs is appended.
-      bool c = false;
+      float dmax = -__builtin_inff();  // (as the quartet test)
 #pragma unroll
       for (int g = 0; g < RG; ++g)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= ts[g][r];
-      if (__ballot(c) == 0) return;
+        for (int r = 0; r < 4; ++r) dmax = fmaxf(dmax, acc[g][r] - ts[g][r]);
+      if (__ballot(dmax >= 0.f) == 0) return;
       refine(tbr, ibase, acc);
       const unsigned below = (1u << m) - 1u;
 #pragma unroll
@@ -825,12 +827,12 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
       // them and the owners reject them.
       const bool fullw = __builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0;
       if (fullw) {
-        bool c = false;
+        float dmax = -__builtin_inff();  // (as the quartet test)
 #pragma unroll
         for (int g = 0; g < RG; ++g)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) c = c || acc[g][r] >= ts[g][r];
-        if (__ballot(c) == 0) return;
+          for (int r = 0; r < 4; ++r) dmax = fmaxf(dmax, acc[g][r] - ts[g][r]);
+        if (__ballot(dmax >= 0.f) == 0) return;
       }
       refine(tbr, ibase, acc);
       bool pr[RG][4];
@@ -874,14 +876,14 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
     }
     const bool vin = ibase + m < n_v;
     if (full) {
-      bool c = false;
+      float dmax = -__builtin_inff();  // (as the quartet test)
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
         const floatx4 s4 = *reinterpret_cast<const floatx4*>(sqs + (w * RG + g) * 16 + 4 * q);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) c = c || (vin && acc[g][r] >= fmaf(-s4[r], nvt, ts[g][r]));
+        for (int r = 0; r < 4; ++r) dmax = fmaxf(dmax, acc[g][r] - fmaf(-s4[r], nvt, ts[g][r]));
       }
-      if (__ballot(c) == 0) return;
+      if (__ballot(vin && dmax >= 0.f) == 0) return;
     }
     refine(tbr, ibase, acc);
 #pragma unroll
@@ -981,32 +983,48 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
             const uint4* tbr = tb + (16 * c + m) * RW;
             const int* bp = tperm + buf * VP + 16 * c;
 #pragma unroll
-            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
-            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {
-              bool any = false;
+            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j], false);
+            if (vb + 16 * (c + NB4) > n_v) {  // (uniform) the last tile: rows past n_v score NaN
 #pragma unroll
-              for (int j = 0; j < NB4; ++j)
+              for (int j = 0; j < NB4; ++j) {
+                const bool past = vb + 16 * (c + j) + m >= n_v;
 #pragma unroll
                 for (int g = 0; g < RG; ++g)
 #pragma unroll
-                  for (int r = 0; r < 4; ++r) any = any || a4[j][g][r] >= ts[g][r];
-              if (__ballot(any) == 0) continue;
+                  for (int r = 0; r < 4; ++r) a4[j][g][r] = past ? __builtin_nanf("") : a4[j][g][r];
+              }
+            }
+            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {
+              // any pair past its row's coarse threshold: max over the blocks, then over
+              // (score - threshold) — straight VALU, no compare-and-branch chain (fmaxf
+              // drops the NaN of rows past n_v; +inf thresholds give -inf)
+              float dmax = -__builtin_inff();
+#pragma unroll
+              for (int g = 0; g < RG; ++g)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  float mx = a4[0][g][r];
+#pragma unroll
+                  for (int j = 1; j < NB4; ++j) mx = fmaxf(mx, a4[j][g][r]);
+                  dmax = fmaxf(dmax, mx - ts[g][r]);
+                }
+              if (__ballot(dmax >= 0.f) == 0) continue;
             }
 #pragma unroll
             for (int j = 0; j < NB4; ++j)
               filter(a4[j], vb + 16 * (c + j), bp + 16 * j, tbr + 16 * j * RW);
           }
         } else {
-        score(tb + m * RW, vb, acc0);
+        score(tb + m * RW, vb, acc0, true);
         // block pairs: issue block c+1's MFMAs, then filter block c
 #pragma unroll 1
         for (int c = 0; c < NC; c += 2) {
           const uint4* tbr = tb + (16 * c + m) * RW;
           const int* bp = tperm + buf * VP + 16 * c;
-          if (NC > 1) score(tbr + 16 * RW, vb + 16 * c + 16, acc1);
+          if (NC > 1) score(tbr + 16 * RW, vb + 16 * c + 16, acc1, true);
           filter(acc0, vb + 16 * c, bp, tbr);
           if (NC > 1) {
-            if (c + 2 < NC) score(tbr + 32 * RW, vb + 16 * c + 32, acc0);
+            if (c + 2 < NC) score(tbr + 32 * RW, vb + 16 * c + 32, acc0, true);
             filter(acc1, vb + 16 * c + 16, bp + 16, tbr + 16 * RW);
           }
         }

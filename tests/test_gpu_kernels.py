@@ -256,10 +256,11 @@ def _degree_data(degrees, n_items, seed):
     return u, i, r
 
 
-DUAL_DEGREES = [1, 2, 7, 15, 16, 17, 31, 32, 33, 40, 48, 63, 64, 65, 66, 90, 96, 97, 128, 129]
+DUAL_DEGREES = [1, 2, 7, 15, 16, 17, 31, 32, 33, 40, 47, 48, 49, 63, 64, 65, 66, 90, 96, 97, 128, 129]
 
 
-@pytest.mark.parametrize("rank,reg", [(33, 0.1), (40, 0.1), (64, 0.1), (65, 0.1), (96, 0.1),
+@pytest.mark.parametrize("rank,reg", [(33, 0.1), (40, 0.1), (48, 0.1), (64, 0.1), (64, 1e-3),
+                                      (64, 1e-4), (65, 0.1), (96, 0.1),
                                       (100, 0.1), (128, 0.1), (65, 1e-3), (80, 1e-3), (95, 1e-3),
                                       (80, 1e-4), (128, 1e-3)])
 def test_dual_short_rows_match_primal_and_oracle(rank, reg):
@@ -300,7 +301,8 @@ def test_dual_short_rows_match_primal_and_oracle(rank, reg):
         assert np.all(U[:, rank:] == 0.0)
         e = rel_row_errs(U[:, :rank], U_ref)
         out[dual] = {f"deg<={b}": float(e[(deg <= b) & (deg > a)].max())
-                     for a, b in ((0, 16), (16, 32), (32, 64), (64, 10 ** 9))}
+                     for a, b in ((0, 16), (16, 32), (32, 48), (48, 64), (64, 10 ** 9))
+                     if ((deg <= b) & (deg > a)).any()}
         assert e.max() <= 1e-4, (dual, out[dual])
     report(f"dual_vs_primal[rank={rank},reg={reg:g}]", out)
 

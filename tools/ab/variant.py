@@ -41,6 +41,9 @@ VARIANTS = {
     # round 6: quad top-k lists (16 < top <= 128) with one row group only
     # round 6: the committed (HEAD) topk.hip in place of the working tree's ("@HEAD" files)
     "oldtopk": [(TK, "@HEAD", None)],
+    # a candidate topk.hip kept outside the tree (/tmp/topk_cand.hip)
+    "tkcand": [(TK, "@FILE", "/tmp/topk_cand.hip")],
+    "tkprev": [(TK, "@FILE", "/tmp/topk_prev.hip")],
     # round 6: the LDL^T pivot-spread limit (rows beyond it go to the fp64 rescue)
     **{f"cond{c}": [(GS, "constexpr float kCondMax = 32.f;", f"constexpr float kCondMax = {c}.f;")]
        for c in (2, 4, 8, 16)},
@@ -344,6 +347,9 @@ def build(tag: str) -> str:
     shutil.copytree(CSRC, src)
     for f, old, new in VARIANTS[tag]:
         p = os.path.join(src, f)
+        if old == "@FILE":  # the whole file from a path (outside the tree: a candidate)
+            shutil.copyfile(new, p)
+            continue
         if old == "@HEAD":  # the whole file as committed
             rel = "recommender-system-using-apache-spark-mllib-_amd/csrc/" + f
             open(p, "w").write(subprocess.check_output(["git", "show", "HEAD:" + rel],

@@ -16,6 +16,9 @@ _pkgload.load()
 from als_mi355x import datasets as D, engine as E  # noqa: E402
 from als_mi355x import _lib as _L  # noqa: E402
 
+if os.environ.get("ALS_AB_DUAL64"):  # dev A/B: the rank 33-64 dual-path limit
+    E.DUAL_MAX_RATINGS_64 = int(os.environ["ALS_AB_DUAL64"])
+
 
 def _lib_loaded():
     """The library actually loaded (ALS_HIP_LIB counts only with ALS_HIP_DEV=1)."""

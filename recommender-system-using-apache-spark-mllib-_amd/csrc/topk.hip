@@ -982,8 +982,25 @@ __global__ __launch_bounds__(64 * tk_nw(TOPR)) void topk_split_kernel(const floa
           for (int c = 0; c < NC; c += NB4) {
             const uint4* tbr = tb + (16 * c + m) * RW;
             const int* bp = tperm + buf * VP + 16 * c;
+            // the quartet's hi.hi scores, k-step outermost: each step's B operands of the
+            // four blocks, then 4 RG independent MFMAs (a dependent MFMA comes 4 RG issues
+            // later, not RG)
 #pragma unroll
-            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j], false);
+            for (int j = 0; j < NB4; ++j)
+#pragma unroll
+              for (int g = 0; g < RG; ++g) a4[j][g] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < NK; ++s) {
+              tk_half8 bh[NB4];
+#pragma unroll
+              for (int j = 0; j < NB4; ++j)
+                bh[j] = __builtin_bit_cast(tk_half8, tbr[16 * j * RW + ((4 * s + q) ^ swz)]);
+#pragma unroll
+              for (int j = 0; j < NB4; ++j)
+#pragma unroll
+                for (int g = 0; g < RG; ++g)
+                  a4[j][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[g][s], bh[j], a4[j][g], 0, 0, 0);
+            }
             if (vb + 16 * (c + NB4) > n_v) {  // (uniform) the last tile: rows past n_v score NaN
 #pragma unroll
               for (int j = 0; j < NB4; ++j) {

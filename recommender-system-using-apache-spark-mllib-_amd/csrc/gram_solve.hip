@@ -1552,16 +1552,20 @@ __device__ __forceinline__ float absmax4(const floatx4& x) {
 constexpr float kWindowT = 0.0625f;  // 2^-4, in scaled units (launch max in [2^14, 2^15))
 
 // Largest diagonal entry of an upper-tile set in the MFMA C layout (this lane's).
+// (Lane (q, m) holds a diagonal entry of each diagonal tile iff r = m - 4q is in [0, 4):
+// one select per tile, not a compare-and-select per (tile, r) — 4 CN + 1 VALU instead
+// of ~4 x 4 CN.)
 template <int CN>
 __device__ __forceinline__ float diag_max_lane(const floatx4 (&A)[CN * (CN + 1) / 2]) {
   const int lane = threadIdx.x & 63, q = lane >> 4, m = lane & 15;
+  const int r = m - 4 * q;
   float d = 0.f;
 #pragma unroll
-  for (int c = 0; c < CN; ++c)
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (4 * q + r == m) d = fmaxf(d, A[tile_index(CN, c, c)][r]);
-  return d;
+  for (int c = 0; c < CN; ++c) {
+    const floatx4& t = A[tile_index(CN, c, c)];
+    d = fmaxf(d, r == 0 ? t[0] : (r == 1 ? t[1] : (r == 2 ? t[2] : t[3])));
+  }
+  return (r >= 0 && r < 4) ? d : 0.f;
 }
 
 // Sum of the diagonal entries of real dims (dims < k) of an upper-tile set in the C

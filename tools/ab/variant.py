@@ -44,6 +44,7 @@ VARIANTS = {
     # a candidate topk.hip kept outside the tree (/tmp/topk_cand.hip)
     "tkcand": [(TK, "@FILE", "/tmp/topk_cand.hip")],
     "tkprev": [(TK, "@FILE", "/tmp/topk_prev.hip")],
+    "gsprev": [(GS, "@FILE", "/tmp/gs_prev.hip")],
     # round 6: the LDL^T pivot-spread limit (rows beyond it go to the fp64 rescue)
     **{f"cond{c}": [(GS, "constexpr float kCondMax = 32.f;", f"constexpr float kCondMax = {c}.f;")]
        for c in (2, 4, 8, 16)},

@@ -44,6 +44,9 @@ VARIANTS = {
     # a candidate topk.hip kept outside the tree (/tmp/topk_cand.hip)
     "tkcand": [(TK, "@FILE", "/tmp/topk_cand.hip")],
     "tkprev": [(TK, "@FILE", "/tmp/topk_prev.hip")],
+    # top-k register lists: six blocks per ballot (logs keep four: their registers)
+    "tk_nb6": [(TK, "constexpr int NB4 = 4;  // blocks per ballot",
+                "constexpr int NB4 = (TOPR > 0 && TOPR <= 16) ? 6 : 4;  // blocks per ballot")],
     "gsprev": [(GS, "@FILE", "/tmp/gs_prev.hip")],
     # round 6: the LDL^T pivot-spread limit (rows beyond it go to the fp64 rescue)
     **{f"cond{c}": [(GS, "constexpr float kCondMax = 32.f;", f"constexpr float kCondMax = {c}.f;")]
@@ -145,16 +148,14 @@ __device__ __forceinline__ float rowgroup_bcast(float x) {
     # top-k logs (round 6) timing bound (no lists: wrong results): the sweep alone, every
     # quartet scored (V stream, LDS, MFMA, barriers), no block filtered
     "tk_sweeponly": [
-        (TK, """            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
-            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {""",
-         """            for (int j = 0; j < NB4; ++j) score(tbr + 16 * j * RW, vb + 16 * (c + j), a4[j]);
-#pragma unroll
+        (TK, """            if (vb + 16 * (c + NB4) > n_v) {  // (uniform) the last tile""",
+         """#pragma unroll
             for (int j = 0; j < NB4; ++j)
 #pragma unroll
               for (int g = 0; g < RG; ++g)
                 asm volatile("" :: "v"(a4[j][g][0]), "v"(a4[j][g][1]), "v"(a4[j][g][2]), "v"(a4[j][g][3]));
             if (true) continue;
-            if (__builtin_amdgcn_readfirstlane(full ? 1 : 0) != 0) {"""),
+            if (vb + 16 * (c + NB4) > n_v) {  // (uniform) the last tile"""),
     ],
     # top-k logs event counters (dev): quartets scored / past the coarse ballot, blocks
     # refined, keys appended, log cuts (als_dev_tk_counters)

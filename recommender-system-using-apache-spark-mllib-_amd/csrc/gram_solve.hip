@@ -2431,6 +2431,17 @@ constexpr int kW1NT = 36;
 constexpr bool kW1Prefetch2 = true;
 constexpr int kW1Slot = (kW1NT * 4 + kW1NB + 1) * 64;  // floats per chunk partial
 constexpr int kW1YtyC = kW1NT * 4 * 64;               // floats of the C-layout YtY table
+// Implicit W1 light rows: the C-layout YtY table is copied into the wave's LDS by
+// LDS-DMA when the row starts (36 KB, landing while the Gram accumulates), past the
+// Gram's 192-word staging area; the solve's LDS (W1Lds, written only after the table
+// has been read) overlaps it.  Read from global at the end instead, the compiler
+// spread the 144 loads per lane over ~20 dependent waits — at one wavefront per SIMD,
+// each an unhidden L2 round trip.  4 x 37.9 KB per CU (one wave per SIMD).
+constexpr int kW1YtyLdsOff = 1024;  // bytes
+constexpr int kW1SmemImplicit =
+    (kW1YtyLdsOff + 4 * kW1YtyC) > (int)sizeof(float) * W1Lds::SIZE ? (kW1YtyLdsOff + 4 * kW1YtyC)
+                                                                    : (int)sizeof(float) * W1Lds::SIZE;
+static_assert(kW1YtyC % 256 == 0, "YtY table in 1 KB LDS-DMA pieces");
 
 // ytyC[(t * 4 + r) * 64 + lane] = fp32 YtY entry of register r of upper tile t.
 __global__ __launch_bounds__(64) void yty_ctab_kernel(const double* __restrict__ yty,
@@ -2516,7 +2527,8 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     int32_t* __restrict__ status, const float* __restrict__ scal, const uint32_t* __restrict__ Ysp,
     int32_t kp, int32_t zero_row, RescueList rl) {
   constexpr int CN = 8, NT = kW1NT;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SmemBytes<CN>::value];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[IMPLICIT ? kW1SmemImplicit
+                                                                      : SmemBytes<CN>::value];
   const int lane = threadIdx.x & 63;
   floatx4 acc[NT];
 #pragma unroll
@@ -2539,7 +2551,13 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
   }
   float inv2;
   float rmax = 0.f;  // explicit: this lane's max |rating| (split window guard)
+  float* ytyL = reinterpret_cast<float*>(smem + kW1YtyLdsOff);  // implicit light rows
   if constexpr (IMPLICIT) {
+    if (chunk < 0) {  // (uniform) the YtY table lands in LDS while the Gram accumulates
+#pragma unroll
+      for (int j = 0; j < kW1YtyC / 256; ++j)
+        __builtin_amdgcn_global_load_lds(ytyC + 256 * j + 4 * lane, ytyL + 256 * j, 16, 0, 0);
+    }
     const int e = split_exponent(scal[0] * __builtin_sqrtf(alpha * scal[1]));
     inv2 = ldexpf(1.f, -2 * e);
     gram_accumulate_split<CN, true>(col, val, pb, pe, Y, ld, k, alpha, ldexpf(1.f, e), acc, bt,
@@ -2579,8 +2597,10 @@ __global__ __launch_bounds__(64, 1) void gram_solve_w1_kernel(
     return;
   }
   wave_lds_sync();  // the Gram's staging words are reused by the solve (one wave)
+  if constexpr (IMPLICIT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the table landed
   const int64_t n_reg = IMPLICIT ? (int64_t)npos : (pe - pb);
-  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, ytyC, smem, k, reg,
+  w1_finish_and_solve<IMPLICIT, kW1NB, IMPLICIT>(acc, inv2, bt, n_reg, IMPLICIT ? ytyL : ytyC,
+                                               smem, k, reg,
                                                X + (int64_t)row * ld, ld, row, rl,
                                                IMPLICIT ? kCondMaxImplicit : kCondMax);
 }

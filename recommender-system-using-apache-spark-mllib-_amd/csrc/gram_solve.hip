@@ -1391,7 +1391,10 @@ __device__ __forceinline__ float sel_mask(float v, float w) {
 // latency leaves the pivot chain for one VALU more per pivot.  A/B round 5
 // (profiles/r05/ab_lookahead.jsonl): configs[3] W1 user rows 96.6 -> 95.2 ms, 271.9 ->
 // 270.1 ms/iter; slower where other waves hide the chain (k <= 64: user launch +0.7 %,
-// dual rows +2.5 %).
+// dual rows +2.5 %).  Round 6: two rows ahead (row p+2's copy is brought up to date after
+// the pivot's row updates, so each ds_bpermute has a whole pivot to land; one DPP fmac
+// more per pivot, still bit-identical): W1 user rows 94.9 -> 93.0 ms, 273.4 -> 271.0
+// ms/iter at 4096-rating tasks (profiles/r06/ab_lookahead2.jsonl).
 template <bool LA = false, class Hook>
 __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself_out) {
   // Bv was just written by the matrix cores (the pivot block's Schur update) and is
@@ -1402,8 +1405,12 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
   float dmin = 3.0e38f;
   float dself = 1.f;
   float rowp = rowgroup_bcast<0>(B[0]);
-  float pre = 0.f;  // LA: the next pivot row's broadcast copy
-  if constexpr (LA) pre = rowgroup_bcast<0>(B[1]);  // row 1 before pivot 0
+  float pre = 0.f;   // LA: the next pivot row's broadcast copy
+  float pre2 = 0.f;  // LA: the one after it (its ds_bpermute has a whole pivot to land)
+  if constexpr (LA) {
+    pre = rowgroup_bcast<0>(B[1]);   // row 1 before pivot 0
+    pre2 = rowgroup_bcast<0>(B[2]);  // row 2 before pivot 0
+  }
   float d = bcast16<0>(rowp);
   float rd = rcp_t(d);
   float f = rowp * rd;
@@ -1422,9 +1429,16 @@ __device__ __forceinline__ float sweep16c(floatx4& Bv, Hook&& hook, float& dself
         nfn = sel_lane16_n<p + 1>(0.f, fn);
       }
       static_for<4>([&](auto rc) { fmac_bcast16<p>(B[decltype(rc)::value], nf); });
-      if constexpr (p + 2 < 16) {  // row p+2 after pivots <= p: consumed by pivot p+1
-        constexpr int q2 = (p + 2) / 4, r2 = (p + 2) % 4;
-        pre = rowgroup_bcast<q2>(B[r2]);
+      // row p+2's copy (broadcast two pivots ago) after pivot p, after this pivot's row
+      // updates so its ds_bpermute has had them to land; row p+3's broadcast (after
+      // pivots <= p) is issued now and consumed two pivots on
+      if constexpr (p + 2 < 16) fmac_bcast16<p>(pre2, nf);
+      if constexpr (p + 3 < 16) {
+        constexpr int q3 = (p + 3) / 4, r3 = (p + 3) % 4;
+        pre = pre2;
+        pre2 = rowgroup_bcast<q3>(B[r3]);
+      } else {
+        pre = pre2;
       }
     } else {
       // the register holding row p+1 first: then pivot p+1's row is final

@@ -48,6 +48,8 @@ VARIANTS = {
     "tk_nb6": [(TK, "constexpr int NB4 = 4;  // blocks per ballot",
                 "constexpr int NB4 = (TOPR > 0 && TOPR <= 16) ? 6 : 4;  // blocks per ballot")],
     "gsprev": [(GS, "@FILE", "/tmp/gs_prev.hip")],
+    # the n x n dual kernel: step s+1's gathers in flight during step s at NB = 6 too
+    "dualnb2": [(GS, "constexpr int NBUF = NB <= 4 ? 2 : 1;", "constexpr int NBUF = 2;")],
     # round 6: the LDL^T pivot-spread limit (rows beyond it go to the fp64 rescue)
     **{f"cond{c}": [(GS, "constexpr float kCondMax = 32.f;", f"constexpr float kCondMax = {c}.f;")]
        for c in (2, 4, 8, 16)},

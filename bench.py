@@ -33,7 +33,12 @@ bytes per launch / event time / 8 TB/s; the same over the kernel-trace average o
 the PMC profiling runs (`frac_pmc_profile`: tools/gpu_pmc.sh, `bench.py --only W
 --steps 3`, a different and shorter run than this one); the PMC traffic / counter DRAM fraction / busy fractions
 / limiter of that workload's own profiled launches (profiles/pmc_summary.json,
-keyed by workload, kernel and grid size).  `cpu_baseline`: the C port of Spark's
+keyed by workload, kernel and grid size).  At N = 1 the headline workload's counters
+are measured by the run itself: before it touches the GPU, bench.py runs
+`bench.py --only c1 --steps 3` under rocprofv3 as five child processes (a kernel
+trace and tools/gpu_pmc.sh's four --pmc counter sets) and folds them over the
+committed configs1 entry (`live_counters`, `roofline.counters_source`;
+`--no-live-pmc` skips it).  `cpu_baseline`: the C port of Spark's
 per-row dspr + dppsv arithmetic (oracle/als_oracle.c) on every host core in this
 process's affinity set, bounded sample, with the Spark probe (java / pyspark)
 recorded.  `--only c1|c2|c3|c4` runs a single workload (profiling passes).
@@ -119,12 +124,88 @@ def gather_bytes(nnz: int, n_rows: int, k: int) -> float:
     return nnz * (4 * k + 8) + n_rows * (4 * k + 8)
 
 
+# workload -> folded counters measured by this bench run (live_counters), over the file's
+_LIVE = {}
+# the counter sets of tools/gpu_pmc.sh, one rocprofv3 pass each (within the gfx950
+# per-pass block limits: <= 8 SQ_, FETCH_SIZE = 3 TCC_, WRITE_SIZE = 2 TCC_, 1 GRBM_)
+LIVE_PASSES = (
+    ("T", ["--kernel-trace"]),
+    ("A", ["--pmc", "GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+           "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_VALU_MFMA_BUSY_CYCLES",
+           "SQ_INSTS_VALU", "SQ_BUSY_CYCLES"]),
+    ("B", ["--pmc", "GRBM_GUI_ACTIVE", "FETCH_SIZE"]),
+    ("C", ["--pmc", "GRBM_GUI_ACTIVE", "WRITE_SIZE"]),
+    ("D", ["--pmc", "GRBM_GUI_ACTIVE", "SQ_INSTS_VALU_MFMA_MOPS_F16",
+           "SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_MFMA",
+           "SQ_WAVES"]),
+)
+
+
 def _pmc_doc():
     try:
         with open(PMC_FILE) as f:
-            return json.load(f)
+            doc = json.load(f)
     except Exception:
-        return {}
+        doc = {}
+    if _LIVE:
+        doc.setdefault("workloads", {}).update(_LIVE)
+    return doc
+
+
+def live_counters(timeout_s: int = 150) -> dict:
+    """The headline workload's counters measured by this run: five child processes
+    `rocprofv3 <pass> -- python3 bench.py --only c1 --steps 3 --warmup 1` (one kernel-trace
+    pass and the four --pmc passes of tools/gpu_pmc.sh), started before this process
+    touches the GPU, folded by tools/pmc_fold.py into _LIVE["configs1"] so the primary
+    line's roofline.traffic / limiter / busy fractions come from this run, not from the
+    committed profiles/pmc_summary.json.  Any failure leaves the committed profile in
+    place and is recorded."""
+    import importlib.util
+    import shutil
+    import subprocess
+    import tempfile
+    rec = {"passes": [p for p, _ in LIVE_PASSES], "workload": "configs1",
+           "command": "bench.py --only c1 --steps 3 --warmup 1 --no-rmse"}
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        rec["error"] = "rocprofv3 not on PATH"
+        return rec
+    t0 = time.perf_counter()
+    tmp = tempfile.mkdtemp(prefix="als_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    cmd_tail = ["--", sys.executable, os.path.join(ROOT, "bench.py"), "--only", "c1",
+                "--steps", "3", "--warmup", "1", "--no-rmse", "--no-live-pmc"]
+    dirs = []
+    try:
+        for tag, opts in LIVE_PASSES:
+            d = os.path.join(tmp, tag)
+            with open(d + ".log", "w") as log:
+                rc = subprocess.run(["timeout", "-s", "KILL", str(timeout_s), prof] + opts +
+                                    ["-d", d, "-o", "run", "--output-format", "csv"] + cmd_tail,
+                                    cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT,
+                                    ).returncode
+            if rc != 0:
+                with open(d + ".log") as log:
+                    rec["error"] = f"pass {tag} rc {rc}: " + log.read()[-300:]
+                return rec
+            dirs.append(d)
+        spec = importlib.util.spec_from_file_location(
+            "pmc_fold", os.path.join(ROOT, "tools", "pmc_fold.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        folded = mod.fold(dirs)
+        if not folded.get(dominant_kernel(64, False)):
+            rec["error"] = "no counters of the dominant kernel in the passes"
+            return rec
+        _LIVE["configs1"] = folded
+        rec["ok"] = True
+        return rec
+    except Exception as e:  # the primary line must still print
+        rec["error"] = f"{type(e).__name__}: {e}"[:300]
+        return rec
+    finally:
+        rec["seconds"] = time.perf_counter() - t0
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def load_pmc(workload: str, kernel: str, grid=None):
@@ -265,10 +346,14 @@ def roofline(workload: str, kernel: str, launches: dict, k: int, implicit: bool)
                                     "dense MFMA peak, a unit this kernel does not issue (it runs "
                                     "split-f16 MFMA: see mfma_view); not the roofline"},
     })
-    # where the counter fields come from: separate rocprofv3 --pmc passes of this workload
-    # (not this run), folded into the committed summary
-    out["counters_source"] = ("profiles/pmc_summary.json: rocprofv3 --pmc passes of this "
-                              "workload (tools/gpu_pmc.sh), not measured in this run")
+    # where the counter fields come from: this run's own rocprofv3 child passes
+    # (live_counters), else separate passes folded into the committed summary
+    out["counters_source"] = (
+        "measured by this bench run: rocprofv3 --kernel-trace + 4 --pmc child passes of "
+        "`bench.py --only c1 --steps 3 --warmup 1` before the timed run (bench.live_counters)"
+        if workload in _LIVE else
+        "profiles/pmc_summary.json: rocprofv3 --pmc passes of this workload "
+        "(tools/gpu_pmc.sh), not measured in this run")
     busy = {k_: x / te for k_, x in busy_w.items()} if busy_w else {}
     if busy:
         out["limiter"] = max(busy, key=busy.get)
@@ -645,7 +730,7 @@ def big_single(args, dev, want_c3=True, want_c4=True):
     return c3, c4
 
 
-def run_single(args):
+def run_single(args, live=None):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     if args.only in ("c3", "c4"):
@@ -696,6 +781,7 @@ def run_single(args):
                    "rank": k, "regParam": args.reg, "implicitPrefs": imp, "alpha": alpha,
                    "parallelism": "dp1"},
         "roofline": roof,
+        "live_counters": live,
         "dual": dual,
         "library": library_record(),
         "topk10_recs_per_s": core.n_users / (topk_ms * 1e-3),
@@ -908,13 +994,19 @@ def main():
                     help="profiling runs: only this workload (c4 fits c3 untimed first)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the sharded (RCCL) code path even with one rank")
+    ap.add_argument("--no-live-pmc", dest="live_pmc", action="store_false",
+                    help="N = 1: skip the rocprofv3 child passes that measure the headline "
+                         "kernel's counters in this run (the committed profile is used)")
     args = ap.parse_args()
     if args.only == "c1":
         args.big, args.cpu_baseline = False, False
     if args.gpus > 1 or int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.force_dist:
         run_distributed(args)
     else:
-        run_single(args)
+        # before this process touches the GPU: the child passes get the card to themselves
+        live = live_counters() if (args.live_pmc and args.only is None and args.rank == 64
+                                   and not args.implicit and args.config == "ml25m") else None
+        run_single(args, live)
 
 
 if __name__ == "__main__":

@@ -86,3 +86,42 @@ def test_phase_counters_combine_by_grid(bench, monkeypatch):
     (32, 20, 1000, "topk_split_kernel<1,1,32>", 8 * 512)])
 def test_topk_variant_matches_launch_choice(bench, k, top, n_q, kern, grid):
     assert bench.topk_variant(k, top, n_q) == (kern, grid)
+
+
+def test_live_counter_passes_fit_the_per_pass_limits(bench):
+    """Each rocprofv3 --pmc pass bench.live_counters starts stays inside gfx950's per-pass
+    block limits (more in one block: 'error code 38' and a hung profiler): <= 8 SQ_,
+    <= 4 TCC_ (FETCH_SIZE takes 3, WRITE_SIZE 2), <= 2 GRBM_; the kernel-trace pass carries
+    no counters."""
+    tcc_cost = {"FETCH_SIZE": 3, "WRITE_SIZE": 2}
+    tags = [t for t, _ in bench.LIVE_PASSES]
+    assert tags == ["T", "A", "B", "C", "D"]
+    for tag, opts in bench.LIVE_PASSES:
+        if tag == "T":
+            assert opts == ["--kernel-trace"]
+            continue
+        assert opts[0] == "--pmc" and "--sys-trace" not in opts
+        cnt = opts[1:]
+        assert sum(c.startswith("SQ_") for c in cnt) <= 8
+        assert sum(tcc_cost.get(c, 1 if c.startswith("TCC_") else 0) for c in cnt) <= 4
+        assert sum(c.startswith("GRBM_") for c in cnt) <= 2
+
+
+def test_live_counters_overlay_the_committed_profile(bench, monkeypatch):
+    """Counters folded from this run's passes replace the committed entry of their
+    workload only, and the roofline names where its counters came from."""
+    monkeypatch.setattr(bench, "_LIVE", {"configs1": {"gram_solve_kernel<4,false>": {
+        "by_grid": {"640": {"FETCH_SIZE": 1.0, "fetch_bytes_x2": 2048.0, "write_bytes": 0.0,
+                            "pmc_run_avg_ns": 1000.0}}}}})
+    assert bench.load_pmc("configs1", "gram_solve_kernel<4,false>", 640)["fetch_bytes_x2"] == 2048.0
+    doc = bench._pmc_doc()
+    assert "configs2" in doc.get("workloads", {}) or not os.path.exists(bench.PMC_FILE)
+    r = bench.roofline("configs1", "gram_solve_kernel<4,false>",
+                       {"item": {"ms": 1.0, "nnz": 1000, "rows": 10,
+                                 "parts": [("gram_solve_kernel<4,false>", 640)]}}, 64, False)
+    assert r["counters_source"].startswith("measured by this bench run")
+    assert r["traffic"] == 2048.0
+    r2 = bench.roofline("configs2", "gram_solve_w1_kernel<true>",
+                        {"item": {"ms": 1.0, "nnz": 1000, "rows": 10,
+                                  "parts": [("gram_solve_w1_kernel<true>", 640)]}}, 128, True)
+    assert r2["counters_source"].startswith("profiles/pmc_summary.json")

@@ -575,10 +575,10 @@ def _half_sweep_timed(core, block, Y, X, k, reg, imp, alpha, yty, ev=None):
 def _iteration(core, k, reg, imp, alpha, evs=None):
     """One ALS iteration in Spark's order (ALS.train loop): items from users, then users
     from items; implicit: YtY of the source side before each half-sweep (computeYtY)."""
-    yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
+    yty = E.compute_yty(core.U, core.n_users, k, core.ws_yty) if imp else None
     _half_sweep_timed(core, core.item_block, core.U, core.V, k, reg, imp, alpha, yty,
                       evs[0:3] if evs else None)
-    yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
+    yty = E.compute_yty(core.V, core.n_items, k, core.ws_yty) if imp else None
     _half_sweep_timed(core, core.user_block, core.V, core.U, k, reg, imp, alpha, yty,
                       evs[3:6] if evs else None)
 
@@ -630,7 +630,7 @@ def rescued_rows(core, k, reg, imp, alpha):
     out = {}
     for name, block, Y, X, n_src in (("item", core.item_block, core.U, core.V, core.n_users),
                                      ("user", core.user_block, core.V, core.U, core.n_items)):
-        yty = E.compute_yty(Y, n_src, k, core.ws) if imp else None
+        yty = E.compute_yty(Y, n_src, k, core.ws_yty) if imp else None
         E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
                      E.PHASE_ALL & ~E.PHASE_RESCUE)
         torch.cuda.synchronize()

@@ -3165,7 +3165,10 @@ __device__ __forceinline__ void wg_yty_reduce_task(const double* __restrict__ sl
   } while (0)
 
 // Element-wise fp64 sum of the YtY task slots (fixed order: four interleaved
-// partial sums, then combined), so the final reduce reads one slot.
+// partial sums, then combined), so the final reduce reads one slot.  A thread's
+// loads are independent of its adds: 32 are issued per round before the adds
+// consume them in the same order (one round trip per 32 slots, not per 4; a
+// few dozen workgroups run this, so the latency is the kernel's time).
 __global__ __launch_bounds__(256) void slot_sum_kernel(const double* __restrict__ slots,
                                                        int nslots, int64_t slot_len,
                                                        double* __restrict__ out) {
@@ -3173,6 +3176,19 @@ __global__ __launch_bounds__(256) void slot_sum_kernel(const double* __restrict_
   if (e >= slot_len) return;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   int i = 0;
+  constexpr int kBatch = 32;
+  for (; i + kBatch <= nslots; i += kBatch) {
+    double v[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) v[j] = slots[(int64_t)(i + j) * slot_len + e];
+#pragma unroll
+    for (int j = 0; j < kBatch; j += 4) {
+      s0 += v[j];
+      s1 += v[j + 1];
+      s2 += v[j + 2];
+      s3 += v[j + 3];
+    }
+  }
   for (; i + 4 <= nslots; i += 4) {
     s0 += slots[(int64_t)i * slot_len + e];
     s1 += slots[(int64_t)(i + 1) * slot_len + e];

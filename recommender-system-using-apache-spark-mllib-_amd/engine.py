@@ -490,6 +490,9 @@ class ALSCore:
             "cuda", torch.cuda.current_device())
         # both CSR sides hold the same ratings: one rating scale for every half-sweep
         self.ws = Workspace(self.device, shared_rating_scale=True)
+        # computeYtY's task slots in a buffer of their own: written over the solve
+        # workspace they would clobber its rating scale word, re-measured every half-sweep
+        self.ws_yty = Workspace(self.device)
         u = _to_device(users, torch.int32, self.device)
         i = _to_device(items, torch.int32, self.device)
         r = _to_device(ratings, torch.float32, self.device)
@@ -524,6 +527,7 @@ class ALSCore:
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.ws = Workspace(self.device)
+        self.ws_yty = self.ws
         self.nnz = 0
         self._auto_chunk = False
         self.user_block = self.item_block = None
@@ -598,13 +602,13 @@ class ALSCore:
 
     def half_sweep_items(self, reg, implicit=False, alpha=1.0):
         self.schedule_for(implicit)
-        yty = compute_yty(self.U, self.n_users, self.rank, self.ws) if implicit else None
+        yty = compute_yty(self.U, self.n_users, self.rank, self.ws_yty) if implicit else None
         solve_half(self.item_block, self.U, self.V, self.rank, reg, implicit, alpha, yty,
                    self.status, self.ws)
 
     def half_sweep_users(self, reg, implicit=False, alpha=1.0):
         self.schedule_for(implicit)
-        yty = compute_yty(self.V, self.n_items, self.rank, self.ws) if implicit else None
+        yty = compute_yty(self.V, self.n_items, self.rank, self.ws_yty) if implicit else None
         solve_half(self.user_block, self.V, self.U, self.rank, reg, implicit, alpha, yty,
                    self.status, self.ws)
 

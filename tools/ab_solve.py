@@ -35,7 +35,7 @@ def parity(core, k, reg, imp, alpha, n_rows=3000):
     worst = 0.0
     for block, Y, X in ((core.item_block, core.U, core.V), (core.user_block, core.V, core.U)):
         Y0 = Y[:, :k].cpu().numpy()
-        yty = E.compute_yty(Y, Y.shape[0], k, core.ws) if imp else None
+        yty = E.compute_yty(Y, Y.shape[0], k, core.ws_yty) if imp else None
         E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws)
         torch.cuda.synchronize()
         deg = (block.row_ptr[1:] - block.row_ptr[:-1])
@@ -91,9 +91,9 @@ def main():
                 ev.setdefault(f"{name}_{tag}", []).append((a, b))
 
     def it(rec):
-        yty = E.compute_yty(core.U, core.n_users, k, core.ws) if imp else None
+        yty = E.compute_yty(core.U, core.n_users, k, core.ws_yty) if imp else None
         half(core.item_block, core.U, core.V, yty, "item", rec)
-        yty = E.compute_yty(core.V, core.n_items, k, core.ws) if imp else None
+        yty = E.compute_yty(core.V, core.n_items, k, core.ws_yty) if imp else None
         half(core.user_block, core.V, core.U, yty, "user", rec)
 
     for _ in range(warm):
@@ -108,7 +108,7 @@ def main():
     rescued = {}
     for name, block, Y, X, n_src in (("item", core.item_block, core.U, core.V, core.n_users),
                                      ("user", core.user_block, core.V, core.U, core.n_items)):
-        yty = E.compute_yty(Y, n_src, k, core.ws) if imp else None
+        yty = E.compute_yty(Y, n_src, k, core.ws_yty) if imp else None
         E.solve_half(block, Y, X, k, reg, imp, alpha, yty, core.status, core.ws,
                      E.PHASE_ALL & ~E.PHASE_RESCUE)
         torch.cuda.synchronize()

@@ -167,6 +167,11 @@ def live_counters(timeout_s: int = 150) -> dict:
     rec = {"passes": [p for p, _ in LIVE_PASSES], "workload": "configs1",
            "command": "bench.py --only c1 --steps 3 --warmup 1 --no-rmse"}
     prof = shutil.which("rocprofv3")
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        # this run is itself profiled (rocprofv3 ... -- python3 bench.py): its children
+        # would inherit the profiler's environment; the profile is the counter source
+        rec["skipped"] = "run under rocprofv3 (ROCPROF* in the environment)"
+        return rec
     if prof is None:
         rec["error"] = "rocprofv3 not on PATH"
         return rec

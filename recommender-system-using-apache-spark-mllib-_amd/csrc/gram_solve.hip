@@ -49,7 +49,14 @@ namespace als {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-constexpr int kYtyChunk = 512;       // src rows per YtY task (>= 256 tasks at 128K rows)
+// src rows per YtY task: a multiple of 32 sized for ~kYtyTasks tasks (two resident
+// workgroups per CU, so every task runs in one round: at 512-row tasks a 162k-row
+// side left 62 CUs with two tasks and 194 with one, a 59k-row side 140 CUs idle)
+constexpr int kYtyTasks = 512;
+__host__ __device__ inline int64_t yty_chunk(int64_t n) {
+  const int64_t c = (n + kYtyTasks - 1) / kYtyTasks;
+  return c < 32 ? 32 : (c + 31) / 32 * 32;
+}
 // workgroups walking the rescue list (rescue64_kernel).  64, not 256: an empty list (the
 // usual case) still costs one finished-block atomic per workgroup on one word; configs[1]
 // LAUNCH2 + RESCUE phases 3 us shorter per half-sweep (profiles/r05/ab_rescue_grid.jsonl).
@@ -3085,8 +3092,9 @@ __global__ __launch_bounds__(64, 2) void yty_partial_kernel(const float* __restr
   double a64[NT][4], b64[CN];
   zero_acc<NT, CN, double>(a64, b64);
   int npos = 0;
-  const int64_t pb = (int64_t)blockIdx.x * kYtyChunk;
-  const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
+  const int64_t chunk = yty_chunk(n);
+  const int64_t pb = (int64_t)blockIdx.x * chunk;
+  const int64_t pe = pb + chunk < n ? pb + chunk : n;
   gram_accumulate<CN, false, true, double>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64, b64,
                                            npos);
   store_slot<NT, CN, double>(slots + (int64_t)blockIdx.x * Cfg<CN>::SLOT, a64, b64, (float)npos);
@@ -3121,8 +3129,9 @@ __device__ __forceinline__ void wg_yty_partial_task(const float* __restrict__ Y,
   double a64[TS::N][4], b64[TS::NRA];
   zero_acc<TS::N, TS::NRA, double>(a64, b64);
   int npos = 0;
-  const int64_t pb = (int64_t)blockIdx.x * kYtyChunk;
-  const int64_t pe = pb + kYtyChunk < n ? pb + kYtyChunk : n;
+  const int64_t chunk = yty_chunk(n);
+  const int64_t pb = (int64_t)blockIdx.x * chunk;
+  const int64_t pe = pb + chunk < n ? pb + chunk : n;
   gram_accumulate<kWgNB, false, true, double, TS>(nullptr, nullptr, pb, pe, Y, ld, k, 0.f, a64,
                                                   b64, npos);
   store_slot<TS::N, TS::NRA, double>(slots + (int64_t)blockIdx.x * kWgSlot + R * kWgSub, a64, b64,
@@ -3164,39 +3173,39 @@ __device__ __forceinline__ void wg_yty_reduce_task(const double* __restrict__ sl
     else CALL(3);                                                         \
   } while (0)
 
-// Element-wise fp64 sum of the YtY task slots (fixed order: four interleaved
-// partial sums, then combined), so the final reduce reads one slot.  A thread's
-// loads are independent of its adds: 32 are issued per round before the adds
-// consume them in the same order (one round trip per 32 slots, not per 4; a
-// few dozen workgroups run this, so the latency is the kernel's time).
-__global__ __launch_bounds__(256) void slot_sum_kernel(const double* __restrict__ slots,
-                                                       int nslots, int64_t slot_len,
-                                                       double* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= slot_len) return;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  int i = 0;
-  constexpr int kBatch = 32;
-  for (; i + kBatch <= nslots; i += kBatch) {
-    double v[kBatch];
+// Element-wise fp64 sum of the YtY task slots, so the final reduce reads one slot.
+// A workgroup owns 64 consecutive elements (one per lane, coalesced) and 16
+// wavefronts: wave w sums slots w, w + 16, ... (8 loads in flight per round),
+// then wave 0 adds the 16 partials in wave order — a fixed order, so the result
+// is deterministic.  (One thread per element over every slot left a few dozen
+// workgroups waiting on one load round trip per 4 slots: 43 us at 318 slots.)
+constexpr int kSlotSumWaves = 16;
+__global__ __launch_bounds__(64 * kSlotSumWaves) void slot_sum_kernel(
+    const double* __restrict__ slots, int nslots, int64_t slot_len, double* __restrict__ out) {
+  __shared__ double part[kSlotSumWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (e < slot_len) {
+    constexpr int kBatch = 8;
+    int i = w;
+    for (; i + kSlotSumWaves * (kBatch - 1) < nslots; i += kSlotSumWaves * kBatch) {
+      double v[kBatch];
 #pragma unroll
-    for (int j = 0; j < kBatch; ++j) v[j] = slots[(int64_t)(i + j) * slot_len + e];
+      for (int j = 0; j < kBatch; ++j) v[j] = slots[(int64_t)(i + kSlotSumWaves * j) * slot_len + e];
 #pragma unroll
-    for (int j = 0; j < kBatch; j += 4) {
-      s0 += v[j];
-      s1 += v[j + 1];
-      s2 += v[j + 2];
-      s3 += v[j + 3];
+      for (int j = 0; j < kBatch; ++j) s += v[j];
     }
+    for (; i < nslots; i += kSlotSumWaves) s += slots[(int64_t)i * slot_len + e];
   }
-  for (; i + 4 <= nslots; i += 4) {
-    s0 += slots[(int64_t)i * slot_len + e];
-    s1 += slots[(int64_t)(i + 1) * slot_len + e];
-    s2 += slots[(int64_t)(i + 2) * slot_len + e];
-    s3 += slots[(int64_t)(i + 3) * slot_len + e];
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && e < slot_len) {
+    double t = part[0][lane];
+#pragma unroll
+    for (int j = 1; j < kSlotSumWaves; ++j) t += part[j][lane];
+    out[e] = t;
   }
-  for (; i < nslots; ++i) s0 += slots[(int64_t)i * slot_len + e];
-  out[e] = (s0 + s1) + (s2 + s3);
 }
 
 __global__ __launch_bounds__(256, 2) void yty_partial_wg_kernel(const float* __restrict__ Y,
@@ -3457,7 +3466,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
 }
 
 size_t als_yty_workspace_bytes(int64_t n, int32_t k) {
-  const int64_t nslots = n > 0 ? (n + kYtyChunk - 1) / kYtyChunk : 1;
+  const int64_t nslots = n > 0 ? (n + yty_chunk(n) - 1) / yty_chunk(n) : 1;
   // task slots + their element-wise sum
   return align_up(sizeof(double) * yty_slot_doubles(k) * (size_t)(nslots + 1)) + 256;
 }
@@ -3473,7 +3482,7 @@ int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed
               "als_yty: workspace too small");
   hipStream_t st = as_stream(stream);
   double* slots = static_cast<double*>(ws);
-  const int nslots = n > 0 ? (int)((n + kYtyChunk - 1) / kYtyChunk) : 0;
+  const int nslots = n > 0 ? (int)((n + yty_chunk(n) - 1) / yty_chunk(n)) : 0;
   const int cn = cn_for_k(k);
   if (nslots == 0) {
     const int kp = 16 * cn;
@@ -3483,7 +3492,8 @@ int als_yty(const float* Y, int64_t n, int32_t ld, int32_t k, double* yty_packed
   const int64_t slen = (int64_t)yty_slot_doubles(k);
   double* ssum = slots + (int64_t)nslots * slen;
   auto sum_slots = [&]() -> int {
-    slot_sum_kernel<<<(unsigned)((slen + 255) / 256), 256, 0, st>>>(slots, nslots, slen, ssum);
+    slot_sum_kernel<<<(unsigned)((slen + 63) / 64), 64 * kSlotSumWaves, 0, st>>>(slots, nslots, slen,
+                                                                               ssum);
     ALS_LAUNCH_CHECK();
     return ALS_OK;
   };

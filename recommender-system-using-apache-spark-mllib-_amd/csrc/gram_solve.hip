@@ -2862,40 +2862,69 @@ __global__ __launch_bounds__(64, 2) void gram_solve_dual_kernel(
 // one thread per slot element; fixed order: four interleaved partial sums),
 // the implicit YtY added in fp64, then rounded once to fp32 into the row's first
 // slot (each thread reads and writes only its own element: in place is safe).
+// Four consecutive elements per thread (16-B loads and stores: the slots are
+// 16-B aligned and kW1Slot is a multiple of 4), each with the same four partial
+// sums in the same order as one element per thread.
 template <bool IMPLICIT>
 __global__ __launch_bounds__(256) void heavy_sum_w1_kernel(const int32_t* __restrict__ slot_begin,
                                                            const int32_t* __restrict__ slot_begin2,
                                                            float* __restrict__ slots,
                                                            const double* __restrict__ yty) {
   constexpr int CN = 8, NT = kW1NT, NE = (NT * 4 + CN + 1) * 64;
+  static_assert(NE % 4 == 0 && kW1Slot % 4 == 0, "heavy_sum_w1: float4 elements");
   const int h = blockIdx.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int e = 4 * (blockIdx.x * 256 + threadIdx.x);
   if (e >= NE) return;
   const SlotRange sr = slot_range(slot_begin, slot_begin2, h);
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  auto ld4 = [&](int i) -> float4 {
+    return *reinterpret_cast<const float4*>(slots + (int64_t)sr.at(i) * kW1Slot + e);
+  };
+  double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
+  double a2[4] = {0.0, 0.0, 0.0, 0.0}, a3[4] = {0.0, 0.0, 0.0, 0.0};
+  auto add = [](double (&a)[4], const float4& x) {
+    a[0] += (double)x.x;
+    a[1] += (double)x.y;
+    a[2] += (double)x.z;
+    a[3] += (double)x.w;
+  };
   int i = 0;
   for (; i + 4 <= sr.n; i += 4) {
-    a0 += (double)slots[(int64_t)sr.at(i) * kW1Slot + e];
-    a1 += (double)slots[(int64_t)sr.at(i + 1) * kW1Slot + e];
-    a2 += (double)slots[(int64_t)sr.at(i + 2) * kW1Slot + e];
-    a3 += (double)slots[(int64_t)sr.at(i + 3) * kW1Slot + e];
+    const float4 x0 = ld4(i), x1 = ld4(i + 1), x2 = ld4(i + 2), x3 = ld4(i + 3);
+    add(a0, x0);
+    add(a1, x1);
+    add(a2, x2);
+    add(a3, x3);
   }
-  for (; i < sr.n; ++i) a0 += (double)slots[(int64_t)sr.at(i) * kW1Slot + e];
-  double v = (a0 + a1) + (a2 + a3);
-  const int ent = e >> 6;
+  for (; i < sr.n; ++i) add(a0, ld4(i));
+  const int ent = e >> 6;  // e .. e + 3 share one entry (64 elements per entry)
+  float o[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) o[c] = (float)((a0[c] + a1[c]) + (a2[c] + a3[c]));
   if (!IMPLICIT && ent == NT * 4 + CN) {  // the chunks' scaled max |rating|: max, not sum
-    float mx = 0.f;
-    for (i = 0; i < sr.n; ++i) mx = fmaxf(mx, slots[(int64_t)sr.at(i) * kW1Slot + e]);
-    v = mx;
+    float mx[4] = {0.f, 0.f, 0.f, 0.f};
+    for (i = 0; i < sr.n; ++i) {
+      const float4 x = ld4(i);
+      mx[0] = fmaxf(mx[0], x.x);
+      mx[1] = fmaxf(mx[1], x.y);
+      mx[2] = fmaxf(mx[2], x.z);
+      mx[3] = fmaxf(mx[3], x.w);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = mx[c];
   }
   if (IMPLICIT && ent < NT * 4) {
-    const int t = ent >> 2, r = ent & 3, lane = e & 63;
-    const int i = (4 * (lane >> 4) + r) * CN + FullTiles<CN>::l1(t);
-    const int j = (lane & 15) * CN + FullTiles<CN>::l2(t);
-    const int hi = i > j ? i : j, lo = i > j ? j : i;
-    v += yty[hi * (hi + 1) / 2 + lo];
+    const int t = ent >> 2, r = ent & 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int lane = (e + c) & 63;
+      const int ii = (4 * (lane >> 4) + r) * CN + FullTiles<CN>::l1(t);
+      const int jj = (lane & 15) * CN + FullTiles<CN>::l2(t);
+      const int hi = ii > jj ? ii : jj, lo = ii > jj ? jj : ii;
+      o[c] = (float)(((a0[c] + a1[c]) + (a2[c] + a3[c])) + yty[hi * (hi + 1) / 2 + lo]);
+    }
   }
-  slots[(int64_t)sr.home() * kW1Slot + e] = (float)v;
+  *reinterpret_cast<float4*>(slots + (int64_t)sr.home() * kW1Slot + e) =
+      make_float4(o[0], o[1], o[2], o[3]);
 }
 
 // Launch 2b: one wavefront per heavy row solves from its summed slot.
@@ -3434,7 +3463,7 @@ int als_solve_half(const int64_t* row_ptr, const int32_t* col, const float* val,
       ALS_LAUNCH_CHECK();                                                                         \
     }                                                                                             \
     if (g2) {                                                                                     \
-      heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot + 255) / 256, g2), 256, 0, st>>>(                 \
+      heavy_sum_w1_kernel<IMP><<<dim3((kW1Slot / 4 + 255) / 256, g2), 256, 0, st>>>(                 \
           heavy_slot_begin, heavy_slot_begin2, slots_f, yty_packed);                              \
       ALS_LAUNCH_CHECK();                                                                         \
       reduce_solve_w1_kernel<IMP><<<g2, 64, 0, st>>>(row_ptr, heavy_rows, heavy_slot_begin,      \
